@@ -1,0 +1,197 @@
+"""Bench: batched SQP-MPC solves/s on MI355X (BASELINE.json metric, config 3: B=4096, N=32).
+
+A "step" = one full SQP_OSQP.sqp solve (<=2 x linearise + QP + line search, src/osqp_sqp.py:76-93)
+of every problem in the per-GPU batch, inputs resident in HBM.  Multi-GPU: one process per GPU
+(torch.distributed.run), each rank solves its own shard (weak scaling, no data-path collective);
+a gloo barrier brackets the timed region and the max time over ranks is reported.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--N 32]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector = FP64 matrix, AMD spec (not in the guide's table)
+
+
+def algorithmic_bytes(N: int):
+    """Compulsory HBM bytes per problem per launch of each kernel (fp64), and per solve
+    (8*(2*(18N-6) + 12 + 3N) = 312 N)."""
+    T = 18 * N - 6
+    lin = (N - 1) * 114 * 8
+    cost = N * 10 * 8
+    return {
+        "solve": 8 * (2 * T + 12 + 3 * N),
+        "k_linearize": 8 * (T + 3 * N) + lin + cost,
+        "k_riccati": 8 * (T + 12) + lin + cost + 8 * T,
+        "k_linesearch": 8 * (2 * T + 3 * N) + 8 * T,
+    }
+
+
+def cpu_baseline(N: int, budget_s: float, seed: int):
+    """The numpy oracle (a port of src/osqp_sqp.py + osqp_solver.py with an exact KKT solve)
+    timed single-threaded on a bounded sample of the same workload."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+    xcur, goals, XU = synthetic_batch(64, N, seed)
+    solver = OSQPSolverRef(N=N)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < 64:
+        SQPRef(solver).sqp(xcur[n], goals[n], XU[n].copy())
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{n} solves (N={N}, seed {seed}) by oracle/osqp_ref.py (numpy+scipy splu, 1 thread) in {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-reps", type=int, default=30)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from indy7_mpc_amd import _lib
+    from indy7_mpc_amd.model import default_model
+    from indy7_mpc_amd.synthetic import make_batch
+
+    B, N = args.batch, args.N
+    T = 18 * N - 6
+    model = default_model()
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local)
+    # a real (non-NULL) torch stream, shared with the library, so torch events bracket our kernels
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    h.set_stream(stream.cuda_stream)
+    seed = 42 + 3 + 1000 * rank  # config 3 (seed = 42 + config index), per-rank shard
+    xcur, goals, XU = make_batch(h, model, B, N, seed)
+    t_xu = torch.from_numpy(XU).to(dev)
+    t_xs = torch.from_numpy(xcur).to(dev)
+    t_goal = torch.from_numpy(goals).to(dev)
+    t_out = torch.empty_like(t_xu)
+    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+
+    def step():
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_goal.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    h.reset_kernel_times()
+    h.set_timing(True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    h.set_timing(False)
+    ktimes = h.kernel_times()
+    step_ms = [a.elapsed_time(b) for a, b in evs]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # iterations actually run (active problems shrink after a break)
+    st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
+    qp_iters_mean = float(st["qp_iters"].mean())
+
+    # B=1 latency (host-to-host, device-resident input)
+    lat = []
+    for i in range(args.latency_reps + 3):
+        torch.cuda.synchronize(dev)
+        a = time.perf_counter()
+        h.solve_device(1, t_xu.data_ptr(), t_xs.data_ptr(), t_goal.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
+        torch.cuda.synchronize(dev)
+        if i >= 3:
+            lat.append((time.perf_counter() - a) * 1e3)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    total = B * world * args.steps
+    value = total / elapsed
+    ab = algorithmic_bytes(N)
+    dom = max(ktimes, key=lambda k: ktimes[k][0])
+    dom_ms, dom_cnt = ktimes[dom]
+    dom_avg_s = dom_ms / max(dom_cnt, 1) / 1e3
+    achieved = B * ab[dom] / dom_avg_s / 1e9
+    per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c, "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)}
+                  for k, (ms, c) in ktimes.items()}
+    out = {
+        "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
+        "value": value,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (random start/goal states, SURVEY.md §8d, seed 45+1000*rank)",
+        "config": {"workload": f"config3: B={B} problems/GPU, N={N}, full SQP (<=2 QP + line search), exact KKT",
+                   "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)"},
+        "p50_latency_ms": statistics.median(step_ms),
+        "p50_latency_b1_ms": statistics.median(lat),
+        "qp_iters_mean": qp_iters_mean,
+        "kernels": per_kernel,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_problem": ab[dom]},
+        "roofline_solve": {"bound": "hbm", "achieved": value * ab["solve"] / 1e9, "peak": HBM_PEAK_GBS * world,
+                           "unit": "GB/s", "frac": value * ab["solve"] / 1e9 / (HBM_PEAK_GBS * world),
+                           "bytes_per_solve": ab["solve"]},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget, seed)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

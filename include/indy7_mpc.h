@@ -1,0 +1,161 @@
+/*
+ * indy7_mpc.h — C-ABI of the MI355X-native batched SQP-MPC solver (libindy7mpc.so).
+ *
+ * Plain C: pointers, sizes, int status codes. No torch / HIP types in any signature
+ * (streams are passed as opaque `void*` = hipStream_t).
+ *
+ * Each entry point replaces a piece of the reference's Python/pinocchio/OSQP hot path
+ * (reference A2R-Lab/indy7-mpc @ 2025-05-23, paths relative to its root):
+ *
+ *   i7m_create / i7m_destroy   OSQPSolver.__init__            src/osqp_solver.py:7-46
+ *                              (dims, costs, templates, osqp.setup once; here: device
+ *                               buffers for max_batch problems, model constants)
+ *   i7m_solve / _device        SQP_OSQP.sqp                   src/osqp_sqp.py:76-93
+ *                              — the whole <=2-iteration SQP (linearise, QP, line search,
+ *                               step) for B independent problems, batch axis of
+ *                               src/gato_mpc_batch.py:38-43,97-99
+ *   i7m_qp                     OSQPSolver.setup_and_solve_qp  src/osqp_solver.py:137-143
+ *                              (returns the QP minimiser sol.x, solved exactly)
+ *   i7m_linearize              update_constraint_matrix + update_cost_matrix
+ *                                                             src/osqp_solver.py:70-135
+ *   i7m_merit                  SQP_OSQP.eepos_cost + integrator_err
+ *                                                             src/osqp_sqp.py:13-47
+ *   i7m_linesearch             SQP_OSQP.linesearch            src/osqp_sqp.py:49-74
+ *   i7m_eepos                  OSQPSolver.eepos / d_eepos     src/osqp_solver.py:146-155
+ *   i7m_aba                    pin.aba (+f_ext)               src/osqp_sqp.py:40, src/utils.py:5
+ *   i7m_aba_derivatives        pin.computeABADerivatives      src/osqp_solver.py:71,76
+ *   i7m_rk4                    utils.rk4 (plant)              src/utils.py:3-18
+ *
+ * Layouts (all fp64, C-contiguous, row = problem):
+ *   XU    (B, T)  T = 18N-6, [x_0,u_0,x_1,u_1,...,x_{N-1}], x=[q(6),v(6)]  src/osqp_solver.py:22
+ *   xcur  (B, 12)
+ *   goals (B, N*goal_stride), goal_stride 3 (OSQP surface, src/osqp_solver.py:111) or
+ *         6 (batch_sqp surface, gato_controller.py:180-183; first 3 of each 6 used)
+ *
+ * Status: 0 = OK, <0 = error (see I7M_E*), message via i7m_last_error() (thread-local).
+ * Threading: a handle is not re-entrant (like the reference's stateful OSQPSolver);
+ * use one handle per (host thread, device).
+ */
+#ifndef INDY7_MPC_H
+#define INDY7_MPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define I7M_NJ 6
+#define I7M_NX 12
+#define I7M_NU 6
+#define I7M_MAX_SQP 8
+#define I7M_MAX_N 64
+
+#define I7M_OK 0
+#define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */
+#define I7M_EHIP -2     /* HIP runtime error */
+#define I7M_ENOMEM -3   /* device allocation failed */
+#define I7M_ENODEV -4   /* no usable gfx950 device */
+
+/* 6-DOF serial chain of revolute joints about local +z. Layout == RobotModel.packed(). */
+typedef struct i7m_model {
+  double placement_R[6][9];   /* joint frame in parent joint frame, row-major */
+  double placement_t[6][3];
+  double mass[6];
+  double com[6][3];           /* in the joint frame */
+  double inertia[6][6];       /* about the COM: xx xy xz yy yz zz */
+  double gravity[3];          /* (0,0,-9.81), src/osqp_mpc.py:8-9 */
+  double q_lower[6], q_upper[6], v_limit[6], effort_limit[6];
+} i7m_model;
+
+enum { I7M_QP_DIRECT = 0 };
+
+typedef struct i7m_config {
+  int32_t N;            /* knot points (<= I7M_MAX_N), default 32   src/osqp_solver.py:7 */
+  int32_t regularize;   /* default 1 */
+  double dt;            /* default 0.01 */
+  double dQ_cost;       /* default 0.01 */
+  double R_cost;        /* default 1e-5 */
+  double QN_cost;       /* default 100 */
+  double eps;           /* default 1 */
+  double mu;            /* merit penalty, 10          src/osqp_sqp.py:50 */
+  double step_tol;      /* SQP break tolerance, 1e-3  src/osqp_sqp.py:90 */
+  int32_t max_sqp_iters;/* 2                          src/osqp_sqp.py:77 */
+  int32_t max_batch;    /* device buffers are sized for this many problems */
+  int32_t device_id;
+  int32_t qp_mode;      /* I7M_QP_DIRECT: exact block-tridiagonal (Riccati) KKT solve */
+  i7m_model model;
+} i7m_config;
+
+/* Per-problem SQP statistics (keys of SQP_OSQP.stats, src/osqp_sqp.py:7-11). */
+typedef struct i7m_problem_stats {
+  int32_t qp_iters;                 /* qp+1 at loop exit                 */
+  int32_t n_alphas;                 /* entries of linesearch_alphas       */
+  int32_t n_steps;                  /* entries of sqp_stepsizes           */
+  int32_t pad;
+  double alphas[I7M_MAX_SQP];
+  double stepsizes[I7M_MAX_SQP];
+} i7m_problem_stats;
+
+typedef struct i7m_handle i7m_handle;
+
+const char* i7m_last_error(void);
+const char* i7m_version(void);
+int i7m_config_default(i7m_config* cfg);          /* fills everything but `model` */
+int i7m_device_count(int* n);
+
+int i7m_create(const i7m_config* cfg, i7m_handle** out);
+void i7m_destroy(i7m_handle* h);
+int i7m_set_stream(i7m_handle* h, void* stream);  /* NULL -> the handle's own stream */
+int i7m_synchronize(i7m_handle* h);
+
+/* Full SQP solve, host buffers in/out (H2D + kernels + D2H, synchronous). */
+int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,
+              int32_t goal_stride, double* xu_out, i7m_problem_stats* stats);
+
+/* Full SQP solve on device-resident buffers, asynchronous on the handle's stream.
+ * d_stats may be NULL. xu_in may alias xu_out (in-place). */
+int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const double* d_xcur,
+                     const double* d_goals, int32_t goal_stride, double* d_xu_out,
+                     i7m_problem_stats* d_stats);
+
+/* One QP (linearise at xu, solve exactly): sol (B, T). */
+int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals,
+           int32_t goal_stride, double* sol);
+
+/* Raw linearisation at xu.  lin (B, N-1, 114): per knot Aq(6x6,row-major, =dt*da/dq),
+ * Av (=I+dt*da/dv), Bu (=dt*Minv), a (=ABA(q,v,u)); cost (B, N, 10): j = J^T e (6),
+ * Qm, dQm, Rm, |e|.  Either output may be NULL. */
+int i7m_linearize(i7m_handle* h, int32_t B, const double* xu, const double* goals, int32_t goal_stride,
+                  double* lin, double* cost);
+
+/* Merit pieces of XU (relative to XU_ref for the initial-state term): out (B, 5) =
+ * qcost, vcost, ucost, integrator_err, |XU[:12]-XU_ref[:12]|. */
+int i7m_merit(i7m_handle* h, int32_t B, const double* xu, const double* xu_ref, const double* goals,
+              int32_t goal_stride, double* out);
+
+/* Backtracking line search of src/osqp_sqp.py:49-74 (no step applied): alpha (B). */
+int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_full,
+                   const double* goals, int32_t goal_stride, double* alpha);
+
+/* Kinematics / dynamics hooks, Bq independent queries (q,v,tau: (Bq,6)). */
+int i7m_eepos(i7m_handle* h, int32_t Bq, const double* q, double* p_out, double* J_out /*(Bq,3,6) or NULL*/);
+int i7m_aba(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau,
+            const double* fext /*(Bq,6) local spatial force on joint 6, or NULL*/, double* a_out);
+int i7m_aba_derivatives(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau,
+                        double* dq /*(Bq,6,6)*/, double* dv, double* Minv, double* a);
+int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* u, double dt,
+            const double* fext, double* q_out, double* v_out);
+
+/* Per-kernel device timing with HIP events on the launch stream. */
+enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_COUNT = 3 };
+int i7m_set_timing(i7m_handle* h, int enable);
+/* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
+int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);
+int i7m_reset_kernel_times(i7m_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* INDY7_MPC_H */

@@ -1,0 +1,578 @@
+// i7m_api.hip — C-ABI of libindy7mpc.so (declared in include/indy7_mpc.h).
+//
+// Host orchestration of the SQP of src/osqp_sqp.py:76-93 on MI355X: per SQP iteration
+// k_linearize -> k_riccati -> k_linesearch on one HIP stream, all buffers device-resident,
+// sized once at i7m_create for max_batch problems (the reference's OSQP setup-once analogue,
+// src/osqp_solver.py:39-41).  No allocation or host sync inside i7m_solve_device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/indy7_mpc.h"
+#include "i7m_kernels.h"
+
+using namespace i7m;
+
+static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                             \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail(I7M_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+struct Timing {
+  int kid;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct i7m_handle {
+  i7m_config cfg;
+  int dev = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  DevModel* d_model = nullptr;
+  // batch buffers (max_batch problems)
+  double *d_xu = nullptr, *d_xs = nullptr, *d_goal = nullptr, *d_sol = nullptr, *d_lin = nullptr,
+         *d_cost = nullptr, *d_kbuf = nullptr, *d_aux = nullptr, *d_out = nullptr;
+  int* d_active = nullptr;
+  ProblemStats* d_stats = nullptr;
+  size_t goal_cap = 0;
+  // timing
+  bool timing = false;
+  std::vector<Timing> ev;
+  std::vector<hipEvent_t> pool;
+  double ms_sum[I7M_K_COUNT] = {0, 0, 0};
+  int counts[I7M_K_COUNT] = {0, 0, 0};
+};
+
+namespace {
+
+DevModel make_dev_model(const i7m_model& m) {
+  DevModel d;
+  std::memset(&d, 0, sizeof(d));
+  for (int i = 0; i < 6; ++i) {
+    for (int k = 0; k < 9; ++k) d.Rp[i][k] = m.placement_R[i][k];
+    for (int k = 0; k < 3; ++k) d.tp[i][k] = m.placement_t[i][k];
+    const double mass = m.mass[i];
+    const double* c = m.com[i];
+    d.m[i] = mass;
+    for (int k = 0; k < 3; ++k) d.h[i][k] = mass * c[k];
+    // inertia about the joint origin: Ic + m (|c|^2 I - c c^T)
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    const double* I = m.inertia[i];
+    d.Io[i][0] = I[0] + mass * (cc - c[0] * c[0]);
+    d.Io[i][1] = I[1] - mass * c[0] * c[1];
+    d.Io[i][2] = I[2] - mass * c[0] * c[2];
+    d.Io[i][3] = I[3] + mass * (cc - c[1] * c[1]);
+    d.Io[i][4] = I[4] - mass * c[1] * c[2];
+    d.Io[i][5] = I[5] + mass * (cc - c[2] * c[2]);
+    d.qlo[i] = m.q_lower[i];
+    d.qhi[i] = m.q_upper[i];
+    d.vlim[i] = m.v_limit[i];
+    d.ulim[i] = m.effort_limit[i];
+  }
+  for (int k = 0; k < 3; ++k) d.g[k] = m.gravity[k];
+  return d;
+}
+
+SolveParams params_of(const i7m_handle* h, int B, int goal_stride) {
+  SolveParams P;
+  P.N = h->cfg.N;
+  P.T = 18 * h->cfg.N - 6;
+  P.B = B;
+  P.goal_stride = goal_stride;
+  P.regularize = h->cfg.regularize;
+  P.max_iters = h->cfg.max_sqp_iters;
+  P.dt = h->cfg.dt;
+  P.dQ = h->cfg.dQ_cost;
+  P.R = h->cfg.R_cost;
+  P.QN = h->cfg.QN_cost;
+  P.eps = h->cfg.eps;
+  P.mu = h->cfg.mu;
+  P.step_tol = h->cfg.step_tol;
+  return P;
+}
+
+int check_batch(const i7m_handle* h, int B, int goal_stride) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (B < 0 || B > h->cfg.max_batch)
+    return fail(I7M_EINVAL, "batch " + std::to_string(B) + " outside [0, max_batch=" +
+                                std::to_string(h->cfg.max_batch) + "]");
+  if (goal_stride != 3 && goal_stride != 6) return fail(I7M_EINVAL, "goal_stride must be 3 or 6");
+  return I7M_OK;
+}
+
+hipEvent_t get_event(i7m_handle* h) {
+  if (!h->pool.empty()) {
+    hipEvent_t e = h->pool.back();
+    h->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+template <class F>
+int timed(i7m_handle* h, int kid, F&& launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (h->timing) {
+    a = get_event(h);
+    b = get_event(h);
+    if (a && b) HIPCHK(hipEventRecord(a, h->stream));
+  }
+  launch();
+  HIPCHK(hipGetLastError());
+  if (h->timing && a && b) {
+    HIPCHK(hipEventRecord(b, h->stream));
+    h->ev.push_back({kid, a, b});
+  }
+  return I7M_OK;
+}
+
+int launch_linearize(i7m_handle* h, const SolveParams& P, const double* xu, const double* goals, const int* active) {
+  const long nthr = (long)P.B * 12 * (P.N - 1);
+  if (nthr == 0) return I7M_OK;
+  const int blk = 256;
+  const int grid = (int)((nthr + blk - 1) / blk);
+  return timed(h, I7M_K_LIN, [&] {
+    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(blk), 0, h->stream, h->d_model, P, xu, goals, active, h->d_lin,
+                       h->d_cost);
+  });
+}
+
+int launch_riccati(i7m_handle* h, const SolveParams& P, const double* xu, const double* xs, const int* active,
+                   double* sol) {
+  if (P.B == 0) return I7M_OK;
+  return timed(h, I7M_K_RICCATI, [&] {
+    hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost, active,
+                       h->d_kbuf, sol);
+  });
+}
+
+int launch_linesearch(i7m_handle* h, const SolveParams& P, double* xu, const double* sol, const double* goals,
+                      int* active, ProblemStats* st, double* alpha_out, int iter, int mode) {
+  if (P.B == 0) return I7M_OK;
+  return timed(h, I7M_K_LINESEARCH, [&] {
+    hipLaunchKernelGGL(k_linesearch, dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals, active, st,
+                       alpha_out, iter, mode);
+  });
+}
+
+// The SQP loop on device buffers (xu updated in place).
+int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double* d_goals, int goal_stride,
+            ProblemStats* d_st) {
+  SolveParams P = params_of(h, B, goal_stride);
+  HIPCHK(hipMemsetAsync(d_st, 0, sizeof(ProblemStats) * (size_t)B, h->stream));
+  // all problems start active
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->d_active), 1, (size_t)B, h->stream));
+  for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
+    int rc;
+    if ((rc = launch_linearize(h, P, d_xu, d_goals, h->d_active))) return rc;
+    if ((rc = launch_riccati(h, P, d_xu, d_xs, h->d_active, h->d_sol))) return rc;
+    if ((rc = launch_linesearch(h, P, d_xu, h->d_sol, d_goals, h->d_active, d_st, nullptr, it, 0))) return rc;
+  }
+  return I7M_OK;
+}
+
+int copy_in(i7m_handle* h, double* dst, const double* src, size_t n) {
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  return I7M_OK;
+}
+int copy_out(i7m_handle* h, double* dst, const double* src, size_t n) {
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  return I7M_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* i7m_last_error(void) { return g_err.c_str(); }
+
+const char* i7m_version(void) { return "indy7_mpc_amd 0.1 (gfx950, fp64)"; }
+
+int i7m_device_count(int* n) {
+  if (!n) return fail(I7M_EINVAL, "null");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(I7M_ENODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *n = c;
+  return I7M_OK;
+}
+
+int i7m_config_default(i7m_config* c) {
+  if (!c) return fail(I7M_EINVAL, "null config");
+  i7m_model keep = c->model;
+  std::memset(c, 0, sizeof(*c));
+  c->model = keep;
+  c->N = 32;
+  c->regularize = 1;
+  c->dt = 0.01;
+  c->dQ_cost = 0.01;
+  c->R_cost = 1e-5;
+  c->QN_cost = 100.0;
+  c->eps = 1.0;
+  c->mu = 10.0;
+  c->step_tol = 1e-3;
+  c->max_sqp_iters = 2;
+  c->max_batch = 1;
+  c->device_id = 0;
+  c->qp_mode = I7M_QP_DIRECT;
+  return I7M_OK;
+}
+
+int i7m_create(const i7m_config* cfg, i7m_handle** out) {
+  if (!cfg || !out) return fail(I7M_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->N < 2 || cfg->N > I7M_MAX_N) return fail(I7M_EINVAL, "N must be in [2, 64]");
+  if (cfg->max_batch < 1) return fail(I7M_EINVAL, "max_batch must be >= 1");
+  if (cfg->max_sqp_iters < 1 || cfg->max_sqp_iters > I7M_MAX_SQP) return fail(I7M_EINVAL, "max_sqp_iters in [1, 8]");
+  if (cfg->qp_mode != I7M_QP_DIRECT) return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (!(cfg->dt > 0.0)) return fail(I7M_EINVAL, "dt must be > 0");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(I7M_ENODEV, "no HIP device available");
+  if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(I7M_EINVAL, "device_id out of range");
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, cfg->device_id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(I7M_ENODEV, std::string("built for gfx950, device is ") + prop.gcnArchName);
+
+  i7m_handle* h = new i7m_handle();
+  h->cfg = *cfg;
+  h->dev = cfg->device_id;
+  auto bail = [&](int rc) {
+    i7m_destroy(h);
+    return rc;
+  };
+  if (hipSetDevice(h->dev) != hipSuccess) return bail(fail(I7M_EHIP, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(I7M_EHIP, "hipStreamCreate failed"));
+  h->stream = h->own;
+  const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
+  // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
+  const size_t scratch = std::max(Bm * T, (size_t)256 * 114);
+  auto alloc = [&](void** p, size_t bytes) -> bool { return hipMalloc(p, bytes ? bytes : 8) == hipSuccess; };
+  bool ok = alloc((void**)&h->d_model, sizeof(DevModel)) && alloc((void**)&h->d_xu, Bm * T * 8) &&
+            alloc((void**)&h->d_xs, Bm * 12 * 8) && alloc((void**)&h->d_goal, Bm * N * 6 * 8) &&
+            alloc((void**)&h->d_sol, scratch * 8) && alloc((void**)&h->d_lin, Bm * (N - 1) * LIN_STRIDE * 8) &&
+            alloc((void**)&h->d_cost, Bm * N * COST_STRIDE * 8) &&
+            alloc((void**)&h->d_kbuf, Bm * (N - 1) * KBUF_STRIDE * 8) && alloc((void**)&h->d_aux, scratch * 8) &&
+            alloc((void**)&h->d_out, scratch * 8) &&
+            alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats));
+  if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
+  DevModel dm = make_dev_model(cfg->model);
+  if (hipMemcpy(h->d_model, &dm, sizeof(dm), hipMemcpyHostToDevice) != hipSuccess)
+    return bail(fail(I7M_EHIP, "model upload failed"));
+  *out = h;
+  return I7M_OK;
+}
+
+void i7m_destroy(i7m_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->dev);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  for (auto& t : h->ev) {
+    hipEventDestroy(t.a);
+    hipEventDestroy(t.b);
+  }
+  for (auto e : h->pool) hipEventDestroy(e);
+  if (h->own) hipStreamDestroy(h->own);
+  delete h;
+}
+
+int i7m_set_stream(i7m_handle* h, void* stream) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  h->stream = stream ? (hipStream_t)stream : h->own;
+  return I7M_OK;
+}
+
+int i7m_synchronize(i7m_handle* h) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const double* d_xcur, const double* d_goals,
+                     int32_t goal_stride, double* d_xu_out, i7m_problem_stats* d_stats) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6;
+  if (d_xu_out != d_xu_in)
+    HIPCHK(hipMemcpyAsync(d_xu_out, d_xu_in, (size_t)B * T * 8, hipMemcpyDeviceToDevice, h->stream));
+  ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
+  return run_sqp(h, B, d_xu_out, d_xcur, d_goals, goal_stride, st);
+}
+
+int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,
+              int32_t goal_stride, double* xu_out, i7m_problem_stats* stats) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu_in || !xcur || !goals || !xu_out) return fail(I7M_EINVAL, "null pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  if ((rc = copy_in(h, h->d_xu, xu_in, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  if ((rc = run_sqp(h, B, h->d_xu, h->d_xs, h->d_goal, goal_stride, h->d_stats))) return rc;
+  if ((rc = copy_out(h, xu_out, h->d_xu, (size_t)B * T))) return rc;
+  if (stats)
+    HIPCHK(hipMemcpyAsync(stats, h->d_stats, sizeof(ProblemStats) * (size_t)B, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals, int32_t goal_stride,
+           double* sol) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu || !xcur || !goals || !sol) return fail(I7M_EINVAL, "null pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  SolveParams P = params_of(h, B, goal_stride);
+  if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  if ((rc = launch_linearize(h, P, h->d_xu, h->d_goal, nullptr))) return rc;
+  if ((rc = launch_riccati(h, P, h->d_xu, h->d_xs, nullptr, h->d_sol))) return rc;
+  if ((rc = copy_out(h, sol, h->d_sol, (size_t)B * T))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_linearize(i7m_handle* h, int32_t B, const double* xu, const double* goals, int32_t goal_stride, double* lin,
+                  double* cost) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu || !goals) return fail(I7M_EINVAL, "null pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  SolveParams P = params_of(h, B, goal_stride);
+  if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  if ((rc = launch_linearize(h, P, h->d_xu, h->d_goal, nullptr))) return rc;
+  if (lin && (rc = copy_out(h, lin, h->d_lin, (size_t)B * (N - 1) * LIN_STRIDE))) return rc;
+  if (cost && (rc = copy_out(h, cost, h->d_cost, (size_t)B * N * COST_STRIDE))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_merit(i7m_handle* h, int32_t B, const double* xu, const double* xu_ref, const double* goals,
+              int32_t goal_stride, double* out) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu || !xu_ref || !goals || !out) return fail(I7M_EINVAL, "null pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  SolveParams P = params_of(h, B, goal_stride);
+  if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_aux, xu_ref, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  hipLaunchKernelGGL(k_merit, dim3(B), dim3(64), 0, h->stream, h->d_model, P, h->d_xu, h->d_aux, h->d_goal, h->d_out);
+  HIPCHK(hipGetLastError());
+  if ((rc = copy_out(h, out, h->d_out, (size_t)B * 5))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_full, const double* goals,
+                   int32_t goal_stride, double* alpha) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu || !xu_full || !goals || !alpha) return fail(I7M_EINVAL, "null pointer");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  SolveParams P = params_of(h, B, goal_stride);
+  if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_sol, xu_full, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  if ((rc = launch_linesearch(h, P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1))) return rc;
+  if ((rc = copy_out(h, alpha, h->d_out, (size_t)B))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+// ---- query hooks: chunk through the max_batch*T-sized scratch buffers ----------------------
+static size_t scratch_doubles(const i7m_handle* h) {
+  return std::max((size_t)h->cfg.max_batch * (18 * (size_t)h->cfg.N - 6), (size_t)256 * 114);
+}
+static size_t query_cap(const i7m_handle* h) { return scratch_doubles(h) / 36; }  // <= 36 doubles/query
+
+int i7m_eepos(i7m_handle* h, int32_t Bq, const double* q, double* p_out, double* J_out) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (Bq < 0 || !q || !p_out) return fail(I7M_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t cap = query_cap(h);
+  int rc;
+  for (size_t o = 0; o < (size_t)Bq; o += cap) {
+    const int n = (int)std::min(cap, (size_t)Bq - o);
+    if ((rc = copy_in(h, h->d_aux, q + 6 * o, 6 * (size_t)n))) return rc;
+    hipLaunchKernelGGL(k_eepos, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_model, n, h->d_aux, h->d_sol,
+                       J_out ? h->d_out : nullptr);
+    HIPCHK(hipGetLastError());
+    if ((rc = copy_out(h, p_out + 3 * o, h->d_sol, 3 * (size_t)n))) return rc;
+    if (J_out && (rc = copy_out(h, J_out + 18 * o, h->d_out, 18 * (size_t)n))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return I7M_OK;
+}
+
+int i7m_aba(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau, const double* fext,
+            double* a_out) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (Bq < 0 || !q || !v || !tau || !a_out) return fail(I7M_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t cap = query_cap(h);
+  int rc;
+  for (size_t o = 0; o < (size_t)Bq; o += cap) {
+    const int n = (int)std::min(cap, (size_t)Bq - o);
+    double* dq = h->d_aux;
+    double* dv = h->d_aux + 6 * (size_t)n;
+    double* dtau = h->d_aux + 12 * (size_t)n;
+    double* df = h->d_aux + 18 * (size_t)n;
+    if ((rc = copy_in(h, dq, q + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, dv, v + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, dtau, tau + 6 * o, 6 * (size_t)n))) return rc;
+    if (fext && (rc = copy_in(h, df, fext + 6 * o, 6 * (size_t)n))) return rc;
+    hipLaunchKernelGGL(k_aba, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_model, n, dq, dv, dtau,
+                       fext ? df : nullptr, h->d_sol);
+    HIPCHK(hipGetLastError());
+    if ((rc = copy_out(h, a_out + 6 * o, h->d_sol, 6 * (size_t)n))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return I7M_OK;
+}
+
+int i7m_aba_derivatives(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau, double* dq_out,
+                        double* dv_out, double* Minv_out, double* a_out) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (Bq < 0 || !q || !v || !tau || !dq_out || !dv_out || !Minv_out || !a_out)
+    return fail(I7M_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(h->dev));
+  // outputs need 3*36+6 doubles per query: put them in d_out/d_sol/d_lin regions
+  const size_t cap = scratch_doubles(h) / 114;
+  int rc;
+  for (size_t o = 0; o < (size_t)Bq; o += cap) {
+    const int n = (int)std::min(cap, (size_t)Bq - o);
+    double* iq = h->d_aux;
+    double* iv = h->d_aux + 6 * (size_t)n;
+    double* it = h->d_aux + 12 * (size_t)n;
+    double* oq = h->d_sol;
+    double* ov = h->d_sol + 36 * (size_t)n;
+    double* om = h->d_sol + 72 * (size_t)n;
+    double* oa = h->d_sol + 108 * (size_t)n;
+    if ((rc = copy_in(h, iq, q + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, iv, v + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, it, tau + 6 * o, 6 * (size_t)n))) return rc;
+    const long nthr = 12L * n;
+    hipLaunchKernelGGL(k_abad, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, h->stream, h->d_model, n, iq, iv,
+                       it, oq, ov, om, oa);
+    HIPCHK(hipGetLastError());
+    if ((rc = copy_out(h, dq_out + 36 * o, oq, 36 * (size_t)n))) return rc;
+    if ((rc = copy_out(h, dv_out + 36 * o, ov, 36 * (size_t)n))) return rc;
+    if ((rc = copy_out(h, Minv_out + 36 * o, om, 36 * (size_t)n))) return rc;
+    if ((rc = copy_out(h, a_out + 6 * o, oa, 6 * (size_t)n))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return I7M_OK;
+}
+
+int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* u, double dt,
+            const double* fext, double* q_out, double* v_out) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (Bq < 0 || !q || !v || !u || !q_out || !v_out) return fail(I7M_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t cap = query_cap(h);
+  int rc;
+  for (size_t o = 0; o < (size_t)Bq; o += cap) {
+    const int n = (int)std::min(cap, (size_t)Bq - o);
+    double* iq = h->d_aux;
+    double* iv = h->d_aux + 6 * (size_t)n;
+    double* iu = h->d_aux + 12 * (size_t)n;
+    double* iff = h->d_aux + 18 * (size_t)n;
+    double* oq = h->d_sol;
+    double* ov = h->d_sol + 6 * (size_t)n;
+    if ((rc = copy_in(h, iq, q + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, iv, v + 6 * o, 6 * (size_t)n))) return rc;
+    if ((rc = copy_in(h, iu, u + 6 * o, 6 * (size_t)n))) return rc;
+    if (fext && (rc = copy_in(h, iff, fext + 6 * o, 6 * (size_t)n))) return rc;
+    hipLaunchKernelGGL(k_rk4, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_model, n, iq, iv, iu, dt,
+                       fext ? iff : nullptr, oq, ov);
+    HIPCHK(hipGetLastError());
+    if ((rc = copy_out(h, q_out + 6 * o, oq, 6 * (size_t)n))) return rc;
+    if ((rc = copy_out(h, v_out + 6 * o, ov, 6 * (size_t)n))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  return I7M_OK;
+}
+
+int i7m_set_timing(i7m_handle* h, int enable) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  h->timing = enable != 0;
+  return I7M_OK;
+}
+
+int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (auto& t : h->ev) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, t.a, t.b));
+    h->ms_sum[t.kid] += ms;
+    h->counts[t.kid] += 1;
+    h->pool.push_back(t.a);
+    h->pool.push_back(t.b);
+  }
+  h->ev.clear();
+  for (int i = 0; i < n && i < I7M_K_COUNT; ++i) {
+    if (ms_sum) ms_sum[i] = h->ms_sum[i];
+    if (counts) counts[i] = h->counts[i];
+  }
+  return I7M_OK;
+}
+
+int i7m_reset_kernel_times(i7m_handle* h) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  int rc = i7m_get_kernel_times(h, nullptr, nullptr, 0);
+  if (rc) return rc;
+  for (int i = 0; i < I7M_K_COUNT; ++i) {
+    h->ms_sum[i] = 0;
+    h->counts[i] = 0;
+  }
+  return I7M_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,378 @@
+// i7m_dynamics.h — rigid-body kinematics/dynamics for a 6-DOF revolute-z serial chain,
+// written for one GPU lane (gfx950, fp64): everything is fully unrolled into registers.
+//
+// Replaces the pinocchio calls on the reference hot path (reference paths):
+//   forwardKinematics / oMi[6].translation       src/osqp_solver.py:146-148   -> fk_jac
+//   computeJointJacobians / getJointJacobian     src/osqp_solver.py:150-155   -> fk_jac
+//   aba                                          src/osqp_sqp.py:40           -> forward_dynamics
+//   computeABADerivatives (+data.ddq)            src/osqp_solver.py:71,76     -> rnea<dual> + chol
+// Conventions (pinocchio's): spatial vectors [linear; angular]; joint i frame placed in
+// its parent by (Rp_i Rz(q_i), t_i); gravity enters as base acceleration -g.
+// Derivatives: forward-mode dual numbers through RNEA at (q, v, a) — one tangent direction
+// per lane — then da/dx = -M^-1 dtau/dx (a fixed). Exact to rounding, like pinocchio's
+// analytical ABA derivatives.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace i7m {
+
+// Device-side model: URDF numbers plus precomputed inertia about each joint origin.
+struct DevModel {
+  double Rp[6][9];   // row-major
+  double tp[6][3];
+  double m[6];
+  double h[6][3];    // m * com
+  double Io[6][6];   // inertia about the joint origin: xx xy xz yy yz zz
+  double g[3];
+  double qlo[6], qhi[6], vlim[6], ulim[6];
+};
+
+// ---------------------------------------------------------------- dual numbers
+struct dual {
+  double v, d;
+};
+__device__ __forceinline__ dual mk(double v, double d = 0.0) { return dual{v, d}; }
+__device__ __forceinline__ dual operator+(dual a, dual b) { return {a.v + b.v, a.d + b.d}; }
+__device__ __forceinline__ dual operator-(dual a, dual b) { return {a.v - b.v, a.d - b.d}; }
+__device__ __forceinline__ dual operator-(dual a) { return {-a.v, -a.d}; }
+__device__ __forceinline__ dual operator*(dual a, dual b) { return {a.v * b.v, fma(a.v, b.d, a.d * b.v)}; }
+__device__ __forceinline__ dual operator*(double a, dual b) { return {a * b.v, a * b.d}; }
+__device__ __forceinline__ dual operator*(dual b, double a) { return {a * b.v, a * b.d}; }
+__device__ __forceinline__ dual operator+(dual a, double b) { return {a.v + b, a.d}; }
+
+template <class T> __device__ __forceinline__ T zero();
+template <> __device__ __forceinline__ double zero<double>() { return 0.0; }
+template <> __device__ __forceinline__ dual zero<dual>() { return dual{0.0, 0.0}; }
+template <class T> __device__ __forceinline__ T cst(double x);
+template <> __device__ __forceinline__ double cst<double>(double x) { return x; }
+template <> __device__ __forceinline__ dual cst<dual>(double x) { return dual{x, 0.0}; }
+
+// a x b
+template <class T>
+__device__ __forceinline__ void cross3(const T a[3], const T b[3], T o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// y = Rp^T x   (Rp constant, row-major)
+template <class T>
+__device__ __forceinline__ void rpT(const double* R, const T x[3], T y[3]) {
+  y[0] = R[0] * x[0] + R[3] * x[1] + R[6] * x[2];
+  y[1] = R[1] * x[0] + R[4] * x[1] + R[7] * x[2];
+  y[2] = R[2] * x[0] + R[5] * x[1] + R[8] * x[2];
+}
+// y = Rp x
+template <class T>
+__device__ __forceinline__ void rp(const double* R, const T x[3], T y[3]) {
+  y[0] = R[0] * x[0] + R[1] * x[1] + R[2] * x[2];
+  y[1] = R[3] * x[0] + R[4] * x[1] + R[5] * x[2];
+  y[2] = R[6] * x[0] + R[7] * x[1] + R[8] * x[2];
+}
+
+// Spatial inertia (about joint origin) times motion (l, w): lin = m l - h x w, ang = Io w + h x l
+template <class T>
+__device__ __forceinline__ void inertia_mul(const DevModel& M, int i, const T l[3], const T w[3], T fl[3],
+                                            T fn[3]) {
+  const double m = M.m[i];
+  const double* h = M.h[i];
+  const double* I = M.Io[i];
+  fl[0] = m * l[0] - (h[1] * w[2] - h[2] * w[1]);
+  fl[1] = m * l[1] - (h[2] * w[0] - h[0] * w[2]);
+  fl[2] = m * l[2] - (h[0] * w[1] - h[1] * w[0]);
+  fn[0] = I[0] * w[0] + I[1] * w[1] + I[2] * w[2] + (h[1] * l[2] - h[2] * l[1]);
+  fn[1] = I[1] * w[0] + I[3] * w[1] + I[4] * w[2] + (h[2] * l[0] - h[0] * l[2]);
+  fn[2] = I[2] * w[0] + I[4] * w[1] + I[5] * w[2] + (h[0] * l[1] - h[1] * l[0]);
+}
+
+// Recursive Newton-Euler, local frames. c/s = cos/sin(q). Writes tau.
+// fext6: optional local spatial force (lin, ang) on the last body (pinocchio f_ext[6]).
+template <class T>
+__device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[6], const T qd[6], const T qdd[6],
+                                     bool grav, const double* fext6, T tau[6]) {
+  T vl[3] = {zero<T>(), zero<T>(), zero<T>()};
+  T vw[3] = {zero<T>(), zero<T>(), zero<T>()};
+  T al[3], aw[3] = {zero<T>(), zero<T>(), zero<T>()};
+  al[0] = cst<T>(grav ? -M.g[0] : 0.0);
+  al[1] = cst<T>(grav ? -M.g[1] : 0.0);
+  al[2] = cst<T>(grav ? -M.g[2] : 0.0);
+  T f[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double* R = M.Rp[i];
+    const double* t = M.tp[i];
+    // parent -> child: y = Rz^T Rp^T (x - t x w)
+    T tw[3], x[3], y[3];
+    T tt[3] = {cst<T>(t[0]), cst<T>(t[1]), cst<T>(t[2])};
+    cross3(tt, vw, tw);
+    x[0] = vl[0] - tw[0]; x[1] = vl[1] - tw[1]; x[2] = vl[2] - tw[2];
+    rpT(R, x, y);
+    vl[0] = c[i] * y[0] + s[i] * y[1];
+    vl[1] = c[i] * y[1] - s[i] * y[0];
+    vl[2] = y[2];
+    rpT(R, vw, y);
+    vw[0] = c[i] * y[0] + s[i] * y[1];
+    vw[1] = c[i] * y[1] - s[i] * y[0];
+    vw[2] = y[2];
+    cross3(tt, aw, tw);
+    x[0] = al[0] - tw[0]; x[1] = al[1] - tw[1]; x[2] = al[2] - tw[2];
+    rpT(R, x, y);
+    al[0] = c[i] * y[0] + s[i] * y[1];
+    al[1] = c[i] * y[1] - s[i] * y[0];
+    al[2] = y[2];
+    rpT(R, aw, y);
+    aw[0] = c[i] * y[0] + s[i] * y[1];
+    aw[1] = c[i] * y[1] - s[i] * y[0];
+    aw[2] = y[2];
+    // joint motion: v += S qd ; a += S qdd + v x (S qd)
+    vw[2] = vw[2] + qd[i];
+    al[0] = al[0] + vl[1] * qd[i];
+    al[1] = al[1] - vl[0] * qd[i];
+    aw[0] = aw[0] + vw[1] * qd[i];
+    aw[1] = aw[1] - vw[0] * qd[i];
+    aw[2] = aw[2] + qdd[i];
+    // f = I a + v x* (I v)
+    T hl[3], hn[3], il[3], in_[3], t1[3], t2[3], t3[3];
+    inertia_mul(M, i, vl, vw, hl, hn);
+    inertia_mul(M, i, al, aw, il, in_);
+    cross3(vw, hl, t1);
+    cross3(vw, hn, t2);
+    cross3(vl, hl, t3);
+    f[i][0] = il[0] + t1[0]; f[i][1] = il[1] + t1[1]; f[i][2] = il[2] + t1[2];
+    f[i][3] = in_[0] + t2[0] + t3[0]; f[i][4] = in_[1] + t2[1] + t3[1]; f[i][5] = in_[2] + t2[2] + t3[2];
+  }
+  if (fext6) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f[5][k] = f[5][k] - cst<T>(fext6[k]);
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    tau[i] = f[i][5];
+    if (i > 0) {
+      const double* R = M.Rp[i];
+      const double* t = M.tp[i];
+      // child -> parent: F = Rp Rz f ; N = Rp Rz n + t x F
+      T x[3], F[3], Nn[3], tF[3];
+      x[0] = c[i] * f[i][0] - s[i] * f[i][1];
+      x[1] = s[i] * f[i][0] + c[i] * f[i][1];
+      x[2] = f[i][2];
+      rp(R, x, F);
+      x[0] = c[i] * f[i][3] - s[i] * f[i][4];
+      x[1] = s[i] * f[i][3] + c[i] * f[i][4];
+      x[2] = f[i][5];
+      rp(R, x, Nn);
+      T tt[3] = {cst<T>(t[0]), cst<T>(t[1]), cst<T>(t[2])};
+      cross3(tt, F, tF);
+      f[i - 1][0] = f[i - 1][0] + F[0];
+      f[i - 1][1] = f[i - 1][1] + F[1];
+      f[i - 1][2] = f[i - 1][2] + F[2];
+      f[i - 1][3] = f[i - 1][3] + Nn[0] + tF[0];
+      f[i - 1][4] = f[i - 1][4] + Nn[1] + tF[1];
+      f[i - 1][5] = f[i - 1][5] + Nn[2] + tF[2];
+    }
+  }
+}
+
+// Composite-rigid-body algorithm: joint-space inertia M (lower triangle filled, symmetric).
+__device__ __forceinline__ void crba(const DevModel& Md, const double c[6], const double s[6], double Mq[6][6]) {
+  // composite inertia of body i in frame i: (m, h[3], I[6] about origin)
+  double cm[6], ch[6][3], cI[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    cm[i] = Md.m[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ch[i][k] = Md.h[i][k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cI[i][k] = Md.Io[i][k];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    // column i: F = IC_i S, S = (0; e_z): lin = e_z x h = (-h_y, h_x, 0), ang = I e_z
+    double fl[3] = {-ch[i][1], ch[i][0], 0.0};
+    double fn[3] = {cI[i][2], cI[i][4], cI[i][5]};
+    Mq[i][i] = fn[2];
+#pragma unroll
+    for (int j = i; j >= 1; --j) {
+      // express F (frame j) in frame j-1, then M[j-1][i] = n_z
+      const double* R = Md.Rp[j];
+      const double* t = Md.tp[j];
+      double x[3], F[3], Nn[3];
+      x[0] = c[j] * fl[0] - s[j] * fl[1];
+      x[1] = s[j] * fl[0] + c[j] * fl[1];
+      x[2] = fl[2];
+      rp(R, x, F);
+      x[0] = c[j] * fn[0] - s[j] * fn[1];
+      x[1] = s[j] * fn[0] + c[j] * fn[1];
+      x[2] = fn[2];
+      rp(R, x, Nn);
+      fn[0] = Nn[0] + (t[1] * F[2] - t[2] * F[1]);
+      fn[1] = Nn[1] + (t[2] * F[0] - t[0] * F[2]);
+      fn[2] = Nn[2] + (t[0] * F[1] - t[1] * F[0]);
+      fl[0] = F[0]; fl[1] = F[1]; fl[2] = F[2];
+      Mq[i][j - 1] = fn[2];
+      Mq[j - 1][i] = fn[2];
+    }
+    if (i > 0) {
+      // IC_{i-1} += X_i^* IC_i X_i^{-1}: rotate (R = Rp Rz), then shift by t
+      const double* R = Md.Rp[i];
+      const double* t = Md.tp[i];
+      const double m = cm[i];
+      double hz[3] = {c[i] * ch[i][0] - s[i] * ch[i][1], s[i] * ch[i][0] + c[i] * ch[i][1], ch[i][2]};
+      double hr[3];
+      rp(R, hz, hr);
+      // Rz I Rz^T
+      const double* I = cI[i];
+      const double cc = c[i] * c[i], ss = s[i] * s[i], cs = c[i] * s[i];
+      double A[3][3];
+      A[0][0] = cc * I[0] - 2.0 * cs * I[1] + ss * I[3];
+      A[1][1] = ss * I[0] + 2.0 * cs * I[1] + cc * I[3];
+      A[0][1] = cs * (I[0] - I[3]) + (cc - ss) * I[1];
+      A[0][2] = c[i] * I[2] - s[i] * I[4];
+      A[1][2] = s[i] * I[2] + c[i] * I[4];
+      A[2][2] = I[5];
+      A[1][0] = A[0][1]; A[2][0] = A[0][2]; A[2][1] = A[1][2];
+      // B = Rp A Rp^T
+      double RA[3][3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) RA[r][q] = R[3 * r] * A[0][q] + R[3 * r + 1] * A[1][q] + R[3 * r + 2] * A[2][q];
+      double Bm[3][3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = r; q < 3; ++q) Bm[r][q] = RA[r][0] * R[3 * q] + RA[r][1] * R[3 * q + 1] + RA[r][2] * R[3 * q + 2];
+      const double ht = hr[0] * t[0] + hr[1] * t[1] + hr[2] * t[2];
+      const double tt = t[0] * t[0] + t[1] * t[1] + t[2] * t[2];
+      const double dg = 2.0 * ht + m * tt;
+      const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int r = iu[k][0], q = iu[k][1];
+        double v = Bm[r][q] - (t[r] * hr[q] + hr[r] * t[q]) - m * t[r] * t[q];
+        if (r == q) v += dg;
+        cI[i - 1][k] += v;
+      }
+      ch[i - 1][0] += hr[0] + m * t[0];
+      ch[i - 1][1] += hr[1] + m * t[1];
+      ch[i - 1][2] += hr[2] + m * t[2];
+      cm[i - 1] += m;
+    }
+  }
+}
+
+// In-place Cholesky (lower) of a 6x6 SPD matrix; L[i][j] for j<=i.
+__device__ __forceinline__ void chol6(double A[6][6]) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
+    d = sqrt(d);
+    A[j][j] = d;
+    const double inv = 1.0 / d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double v = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= A[i][k] * A[j][k];
+      A[i][j] = v * inv;
+    }
+  }
+}
+// Solve L L^T x = b in place.
+__device__ __forceinline__ void chol6_solve(const double L[6][6], double b[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double v = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) v -= L[i][k] * b[k];
+    b[i] = v / L[i][i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double v = b[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) v -= L[k][i] * b[k];
+    b[i] = v / L[i][i];
+  }
+}
+
+// a = ABA(q, v, tau[, fext]) = M^-1 (tau - RNEA(q, v, 0)); L returns chol(M).
+__device__ __forceinline__ void forward_dynamics(const DevModel& Md, const double c[6], const double s[6],
+                                                 const double v[6], const double tau[6], const double* fext6,
+                                                 double L[6][6], double a[6]) {
+  crba(Md, c, s, L);
+  chol6(L);
+  double z[6] = {0, 0, 0, 0, 0, 0}, b[6];
+  rnea<double>(Md, c, s, v, z, true, fext6, b);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a[i] = tau[i] - b[i];
+  chol6_solve(L, a);
+}
+
+// Column `d` of the ABA derivatives at (q, v, a): d < 6 -> da/dq_d, 6 <= d < 12 -> da/dv_{d-6}.
+// out = -M^-1 dRNEA/dx_d (a held fixed).
+__device__ __forceinline__ void aba_deriv_column(const DevModel& Md, const double c[6], const double s[6],
+                                                 const double v[6], const double a[6], const double L[6][6],
+                                                 int d, double out[6]) {
+  dual dc[6], ds[6], dv[6], da[6], dt[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const bool isq = (d == i);
+    dc[i] = dual{c[i], isq ? -s[i] : 0.0};
+    ds[i] = dual{s[i], isq ? c[i] : 0.0};
+    dv[i] = dual{v[i], (d - 6 == i) ? 1.0 : 0.0};
+    da[i] = dual{a[i], 0.0};
+  }
+  rnea<dual>(Md, dc, ds, dv, da, true, nullptr, dt);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[i] = -dt[i].d;
+  chol6_solve(L, out);
+}
+
+// World-frame forward kinematics of the joint-6 origin and its LOCAL_WORLD_ALIGNED linear
+// Jacobian (rows 0..2).  J may be null.
+__device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], const double s[6], double p[3],
+                                       double J[3][6]) {
+  double R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  double pos[3] = {0, 0, 0};
+  double zs[6][3], ps[6][3];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double* Rp = Md.Rp[i];
+    const double* t = Md.tp[i];
+    double np[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) np[r] = pos[r] + R[r][0] * t[0] + R[r][1] * t[1] + R[r][2] * t[2];
+    // R <- R Rp Rz(q)
+    double RR[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) RR[r][q] = R[r][0] * Rp[q] + R[r][1] * Rp[3 + q] + R[r][2] * Rp[6 + q];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double x0 = RR[r][0], x1 = RR[r][1];
+      R[r][0] = x0 * c[i] + x1 * s[i];
+      R[r][1] = x1 * c[i] - x0 * s[i];
+      R[r][2] = RR[r][2];
+      zs[i][r] = RR[r][2];
+      ps[i][r] = np[r];
+      pos[r] = np[r];
+    }
+  }
+  p[0] = pos[0]; p[1] = pos[1]; p[2] = pos[2];
+  if (J) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const double d0 = pos[0] - ps[j][0], d1 = pos[1] - ps[j][1], d2 = pos[2] - ps[j][2];
+      J[0][j] = zs[j][1] * d2 - zs[j][2] * d1;
+      J[1][j] = zs[j][2] * d0 - zs[j][0] * d2;
+      J[2][j] = zs[j][0] * d1 - zs[j][1] * d0;
+    }
+  }
+}
+
+}  // namespace i7m

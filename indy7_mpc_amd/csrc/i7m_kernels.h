@@ -1,0 +1,618 @@
+// i7m_kernels.h — the batched SQP-MPC kernels (gfx950, fp64).
+//
+// One SQP iteration of src/osqp_sqp.py:76-93 for B independent problems is three launches:
+//
+//   k_linearize   thread per (problem, knot, direction d<12): ABA + dual-RNEA derivative
+//                 column d of [dt*da/dq | I+dt*da/dv] (+ dt*Minv column, a); the d==0 lanes
+//                 also evaluate the cost linearisation (FK, LOCAL_WORLD_ALIGNED J, weights).
+//                 Replaces src/osqp_solver.py:70-135 (update_constraint_matrix +
+//                 update_cost_matrix).  Fully knot-parallel: B*(N-1)*12 lanes.
+//   k_riccati     one wavefront per problem: exact solve of the equality-constrained QP
+//                 (the KKT system OSQP iterates on, src/osqp_solver.py:137-143) by a
+//                 backward Riccati recursion over 12x12 / 12x6 stage blocks staged in LDS
+//                 and a forward rollout.  Writes sol.x.
+//   k_linesearch  one wavefront per problem, lanes = (candidate alpha, knot): merit of the
+//                 base point and of the backtracking alphas, several candidates per round,
+//                 first-accept rule of src/osqp_sqp.py:58-72, then the SQP step, step-size
+//                 norm and break test (src/osqp_sqp.py:79-91).
+#pragma once
+
+#include "i7m_dynamics.h"
+
+namespace i7m {
+
+constexpr int LIN_STRIDE = 114;   // Aq(36) Av(36) Bu(36) a(6)
+constexpr int COST_STRIDE = 10;   // j(6) Qm dQm Rm |e|
+constexpr int KBUF_STRIDE = 84;   // K(6x12) kff(6) c_v(6)
+constexpr int NALPHA = 8;
+constexpr int MAXN = 64;
+
+struct SolveParams {
+  int N, T, B, goal_stride, regularize, max_iters;
+  double dt, dQ, R, QN, eps, mu, step_tol;
+};
+
+struct ProblemStats {
+  int qp_iters, n_alphas, n_steps, pad;
+  double alphas[8];
+  double stepsizes[8];
+};
+
+__device__ __forceinline__ void sincos6(const double* q, double c[6], double s[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sincos(q[i], &s[i], &c[i]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Cost linearisation of knot k (src/osqp_solver.py:103-135): writes j = J^T e, Qm, dQm, Rm.
+__device__ __forceinline__ void cost_knot(const DevModel& Md, const SolveParams& P, const double* q,
+                                          const double* goal, int k, double* out) {
+  double c[6], s[6], p[3], J[3][6];
+  sincos6(q, c, s);
+  fk_jac(Md, c, s, p, J);
+  const double e0 = p[0] - goal[0], e1 = p[1] - goal[1], e2 = p[2] - goal[2];
+  const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+  const double w = P.regularize ? (1.0 / (fabs(nrm) + P.eps)) : 1.0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) out[j] = e0 * J[0][j] + e1 * J[1][j] + e2 * J[2][j];
+  out[6] = (k == P.N - 1) ? P.QN : 1.0;
+  out[7] = P.dQ * w;
+  out[8] = P.R * w;
+  out[9] = nrm;
+}
+
+__global__ void __launch_bounds__(256) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
+                                                   const double* __restrict__ xu, const double* __restrict__ goals,
+                                                   const int* __restrict__ active, double* __restrict__ lin,
+                                                   double* __restrict__ cost) {
+  const int per = 12 * (P.N - 1);
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = (int)(gid / per);
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  const int r = (int)(gid - (long)b * per);
+  const int k = r / 12;
+  const int d = r - 12 * k;
+  const DevModel& Md = *Mg;
+  const double* X = xu + (long)b * P.T + 18 * k;
+  double q[6], v[6], u[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { q[i] = X[i]; v[i] = X[6 + i]; u[i] = X[12 + i]; }
+  double c[6], s[6], L[6][6], a[6];
+  sincos6(q, c, s);
+  forward_dynamics(Md, c, s, v, u, nullptr, L, a);
+  double col[6];
+  aba_deriv_column(Md, c, s, v, a, L, d, col);
+  double* out = lin + ((long)b * (P.N - 1) + k) * LIN_STRIDE;
+  const double dt = P.dt;
+  if (d < 6) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) out[i * 6 + d] = dt * col[i];
+    // Bu = dt * Minv, column d from a unit solve; symmetric by construction
+    double e[6] = {0, 0, 0, 0, 0, 0};
+    e[d] = 1.0;
+    chol6_solve(L, e);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      if (i <= d) {
+        out[72 + i * 6 + d] = dt * e[i];
+        out[72 + d * 6 + i] = dt * e[i];
+      }
+    }
+    if (d == 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) out[108 + i] = a[i];
+    }
+  } else {
+    const int dd = d - 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) out[36 + i * 6 + dd] = (i == dd ? 1.0 : 0.0) + dt * col[i];
+  }
+  // cost linearisation: knot k by lane d==0, the terminal knot by lane (N-2, d==1)
+  if (d == 0 || (d == 1 && k == P.N - 2)) {
+    const int kc = (d == 0) ? k : P.N - 1;
+    const double* goal = goals + (long)b * P.N * P.goal_stride + (long)kc * P.goal_stride;
+    cost_knot(Md, P, xu + (long)b * P.T + 18 * kc, goal, kc,
+              cost + ((long)b * P.N + kc) * COST_STRIDE);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Riccati: one 64-lane wavefront (= workgroup) per problem.
+__global__ void __launch_bounds__(64) k_riccati(SolveParams P, const double* __restrict__ xu,
+                                                const double* __restrict__ xs, const double* __restrict__ lin,
+                                                const double* __restrict__ cost, const int* __restrict__ active,
+                                                double* __restrict__ kbuf, double* __restrict__ sol) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  const int l = threadIdx.x;
+  const int N = P.N;
+  const double dt = P.dt;
+  __shared__ double sV[144], sv[12], sVA[144], sT[36], ss[12], sG[72], sH[36], sh[6], svA[12], sK[78];
+  __shared__ double sAq[36], sAv[36], sBu[36], sa[6], sc[6], sw[COST_STRIDE], sX[18];
+  const double* X = xu + (long)b * P.T;
+  const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
+  const double* CB = cost + (long)b * N * COST_STRIDE;
+  double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
+
+  // ---- terminal cost-to-go: V = P_{N-1}, v = g_{N-1}
+  if (l < COST_STRIDE) sw[l] = CB[(N - 1) * COST_STRIDE + l];
+  __syncthreads();
+  for (int e = l; e < 144; e += 64) {
+    const int r = e / 12, cc = e - 12 * (e / 12);
+    double val = 0.0;
+    if (r < 6 && cc < 6) val = sw[6] * (sw[r] * sw[cc]);
+    else if (r == cc) val = sw[7];
+    sV[e] = val;
+  }
+  if (l < 12) sv[l] = (l < 6) ? sw[6] * sw[l] : sw[7] * X[18 * (N - 1) + l];
+  __syncthreads();
+
+  // prefetch registers: stage data = lin (114) + cost (10) + XU_k (18) = 142 values
+  double pf0, pf1, pf2;
+  auto fetch = [&](int k, double& a0, double& a1, double& a2) {
+    const int e0 = l, e1 = l + 64, e2 = l + 128;
+    auto get = [&](int e) -> double {
+      if (e < LIN_STRIDE) return LINb[(long)k * LIN_STRIDE + e];
+      if (e < LIN_STRIDE + COST_STRIDE) return CB[k * COST_STRIDE + (e - LIN_STRIDE)];
+      if (e < LIN_STRIDE + COST_STRIDE + 18) return X[18 * k + (e - LIN_STRIDE - COST_STRIDE)];
+      return 0.0;
+    };
+    a0 = get(e0); a1 = get(e1); a2 = get(e2);
+  };
+  auto stash = [&](double a0, double a1, double a2) {
+    auto put = [&](int e, double val) {
+      if (e < 36) sAq[e] = val;
+      else if (e < 72) sAv[e - 36] = val;
+      else if (e < 108) sBu[e - 72] = val;
+      else if (e < 114) sa[e - 108] = val;
+      else if (e < 124) sw[e - 114] = val;
+      else if (e < 142) sX[e - 124] = val;
+    };
+    put(l, a0); put(l + 64, a1); put(l + 128, a2);
+  };
+  fetch(N - 2, pf0, pf1, pf2);
+
+  for (int k = N - 2; k >= 0; --k) {
+    stash(pf0, pf1, pf2);
+    __syncthreads();
+    if (k > 0) fetch(k - 1, pf0, pf1, pf2);
+    // c_v = v + dt a - (Aq q + Av v + Bu u)    (src/osqp_solver.py:76-81)
+    if (l < 6) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc += sAq[l * 6 + j] * sX[j] + sAv[l * 6 + j] * sX[6 + j] + sBu[l * 6 + j] * sX[12 + j];
+      sc[l] = (sX[6 + l] + sa[l] * dt) - acc;
+    }
+    __syncthreads();
+    // ---- step A: VA = V A (144), T = Vvv Bu (36), s = v + V c (12)
+    for (int e = l; e < 192; e += 64) {
+      if (e < 144) {
+        const int r = e / 12, cc = e - 12 * (e / 12);
+        double acc;
+        if (cc < 6) {
+          acc = sV[r * 12 + cc];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sAq[m * 6 + cc];
+        } else {
+          const int c2 = cc - 6;
+          acc = dt * sV[r * 12 + c2];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sAv[m * 6 + c2];
+        }
+        sVA[e] = acc;
+      } else if (e < 180) {
+        const int t = e - 144, r = t / 6, cc = t - 6 * (t / 6);
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sV[(6 + r) * 12 + 6 + m] * sBu[m * 6 + cc];
+        sT[t] = acc;
+      } else {
+        const int r = e - 180;
+        double acc = sv[r];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sc[m];
+        ss[r] = acc;
+      }
+    }
+    __syncthreads();
+    // ---- step B: AtVA (upper 78) -> sV, G (72), H (21 upper), h (6), vA (12)
+    for (int e = l; e < 189; e += 64) {
+      if (e < 78) {
+        // upper-triangular index e -> (r, cc), r <= cc
+        int r = 0, rem = e;
+        while (rem >= 12 - r) { rem -= 12 - r; ++r; }
+        const int cc = r + rem;
+        double acc;
+        if (r < 6) {
+          acc = sVA[r * 12 + cc];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sAq[m * 6 + r] * sVA[(6 + m) * 12 + cc];
+        } else {
+          const int r2 = r - 6;
+          acc = dt * sVA[r2 * 12 + cc];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sAv[m * 6 + r2] * sVA[(6 + m) * 12 + cc];
+        }
+        sV[r * 12 + cc] = acc;
+        sV[cc * 12 + r] = acc;
+      } else if (e < 150) {
+        const int t = e - 78, r = t / 12, cc = t - 12 * (t / 12);
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * sVA[(6 + m) * 12 + cc];
+        sG[t] = acc;
+      } else if (e < 171) {
+        int t = e - 150, r = 0;
+        while (t >= 6 - r) { t -= 6 - r; ++r; }
+        const int cc = r + t;
+        double acc = (r == cc) ? sw[8] : 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * sT[m * 6 + cc];
+        sH[r * 6 + cc] = acc;
+        sH[cc * 6 + r] = acc;
+      } else if (e < 177) {
+        const int r = e - 171;
+        double acc = sw[8] * sX[12 + r];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * ss[6 + m];
+        sh[r] = acc;
+      } else {
+        const int r = e - 177;
+        double acc;
+        if (r < 6) {
+          acc = sw[6] * sw[r] + ss[r];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sAq[m * 6 + r] * ss[6 + m];
+        } else {
+          const int r2 = r - 6;
+          acc = sw[7] * sX[6 + r2] + dt * ss[r2];
+#pragma unroll
+          for (int m = 0; m < 6; ++m) acc += sAv[m * 6 + r2] * ss[6 + m];
+        }
+        svA[r] = acc;
+      }
+    }
+    __syncthreads();
+    // ---- step C: [K | kff] = -H^-1 [G | h]   (13 right-hand sides, one per lane)
+    if (l < 13) {
+      double Lh[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Lh[i][j] = sH[i * 6 + j];
+      chol6(Lh);
+      double rhs[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) rhs[i] = (l < 12) ? sG[i * 12 + l] : sh[i];
+      chol6_solve(Lh, rhs);
+      if (l < 12) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sK[i * 12 + l] = -rhs[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sK[72 + i] = -rhs[i];
+      }
+    }
+    __syncthreads();
+    // ---- step D: V = Q + AtVA + G^T K (upper 78), v = q + A^T s + G^T kff ; store K, kff, c_v
+    for (int e = l; e < 90; e += 64) {
+      if (e < 78) {
+        int r = 0, rem = e;
+        while (rem >= 12 - r) { rem -= 12 - r; ++r; }
+        const int cc = r + rem;
+        double acc = sV[r * 12 + cc];
+        if (r < 6 && cc < 6) acc += sw[6] * (sw[r] * sw[cc]);
+        else if (r == cc) acc += sw[7];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sG[m * 12 + r] * sK[m * 12 + cc];
+        sV[r * 12 + cc] = acc;
+        sV[cc * 12 + r] = acc;
+      } else {
+        const int r = e - 78;
+        double acc = svA[r];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += sG[m * 12 + r] * sK[72 + m];
+        sv[r] = acc;
+      }
+    }
+    for (int e = l; e < KBUF_STRIDE; e += 64) KB[(long)k * KBUF_STRIDE + e] = (e < 78) ? sK[e] : sc[e - 78];
+    __syncthreads();
+  }
+
+  // ---- forward rollout: x_0 = xs; u_k = K x_k + kff; x_{k+1} = A x + B u + c
+  double* S = sol + (long)b * P.T;
+  __shared__ double sx[2][12], su[6];
+  if (l < 12) {
+    const double x0 = xs[(long)b * 12 + l];
+    sx[0][l] = x0;
+    S[l] = x0;
+  }
+  __syncthreads();
+  for (int k = 0; k < N - 1; ++k) {
+    const int cur = k & 1;
+    if (l < 6) {
+      const double* Kk = KB + (long)k * KBUF_STRIDE;
+      double acc = Kk[72 + l];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) acc += Kk[l * 12 + j] * sx[cur][j];
+      su[l] = acc;
+      S[18 * k + 12 + l] = acc;
+    }
+    __syncthreads();
+    if (l < 12) {
+      double nx;
+      if (l < 6) {
+        nx = sx[cur][l] + dt * sx[cur][6 + l];
+      } else {
+        const int i = l - 6;
+        const double* Lk = LINb + (long)k * LIN_STRIDE;
+        double acc = KB[(long)k * KBUF_STRIDE + 78 + i];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc += Lk[i * 6 + j] * sx[cur][j] + Lk[36 + i * 6 + j] * sx[cur][6 + j] + Lk[72 + i * 6 + j] * su[j];
+        nx = acc;
+      }
+      sx[cur ^ 1][l] = nx;
+      S[18 * (k + 1) + l] = nx;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Merit pieces of one knot (src/osqp_sqp.py:13-47): qcost, vcost, ucost, integrator error.
+// x: 18 values of knot k (12 at the last knot), xn: the 12 state values of knot k+1.
+__device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams& P, int k, const double* x,
+                                           const double* xn, const double* goal, double out[4]) {
+  double c[6], s[6], p[3];
+  sincos6(x, c, s);
+  fk_jac(Md, c, s, p, nullptr);
+  const double e0 = p[0] - goal[0], e1 = p[1] - goal[1], e2 = p[2] - goal[2];
+  const double Qm = (k == P.N - 1) ? P.QN : 1.0;
+  out[0] = Qm * (e0 * e0 + e1 * e1 + e2 * e2);
+  double vv = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) vv += x[6 + i] * x[6 + i];
+  out[1] = P.dQ * vv;
+  out[2] = 0.0;
+  out[3] = 0.0;
+  if (k < P.N - 1) {
+    double uu = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) uu += x[12 + i] * x[12 + i];
+    out[2] = P.R * uu;
+    double L[6][6], a[6];
+    forward_dynamics(Md, c, s, x + 6, x + 12, nullptr, L, a);
+    double eq = 0.0, ev = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double dq = (x[i] + x[6 + i] * P.dt) - xn[i];
+      const double dv = (x[6 + i] + a[i] * P.dt) - xn[6 + i];
+      eq += dq * dq;
+      ev += dv * dv;
+    }
+    out[3] = sqrt(eq) + sqrt(ev);
+  }
+}
+
+// Line search (+ step) — one wavefront per problem.  Candidates: 0 = base point (merit of XU
+// itself, src/osqp_sqp.py:52-55), 1..8 = alphas 1, 1/2, ..., 1/128.  R = max(1, 64/N)
+// candidates per round; the first accepted candidate in alpha order wins (identical to the
+// sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha.
+__global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
+                                                   double* __restrict__ xu, const double* __restrict__ sol,
+                                                   const double* __restrict__ goals, int* __restrict__ active,
+                                                   ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
+                                                   int iter, int mode) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  const int l = threadIdx.x;
+  const int N = P.N;
+  const int R = (N >= 64) ? 1 : 64 / N;
+  const int slot = l / N;
+  const int k = l - slot * N;
+  const DevModel& Md = *Mg;
+  double* X = xu + (long)b * P.T;
+  const double* S = sol + (long)b * P.T;
+  __shared__ double part[64][4];
+  __shared__ double merit[9];
+  __shared__ int chosen;
+  const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
+  if (l == 0) chosen = -1;
+  double base = 0.0;
+  int found = -1;
+  for (int c0 = 0; c0 < 1 + NALPHA && found < 0; c0 += R) {
+    const int cand = c0 + slot;
+    if (slot < R && k < N && cand < 1 + NALPHA) {
+      double x[18], xn[12];
+      const int nk = (k < N - 1) ? 18 : 12;
+      if (cand == 0) {
+        for (int i = 0; i < nk; ++i) x[i] = X[18 * k + i];
+        if (k < N - 1)
+          for (int i = 0; i < 12; ++i) xn[i] = X[18 * (k + 1) + i];
+      } else {
+        const double al = alphas[cand - 1];
+        for (int i = 0; i < nk; ++i) x[i] = X[18 * k + i] + al * (S[18 * k + i] - X[18 * k + i]);
+        if (k < N - 1)
+          for (int i = 0; i < 12; ++i) xn[i] = X[18 * (k + 1) + i] + al * (S[18 * (k + 1) + i] - X[18 * (k + 1) + i]);
+      }
+      double o[4];
+      merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride, o);
+      if (k == 0 && cand > 0) {
+        // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
+        double dd = 0.0;
+        for (int i = 0; i < 12; ++i) {
+          const double t = x[i] - X[i];
+          dd += t * t;
+        }
+        o[3] += sqrt(dd);
+      }
+      part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
+    }
+    __syncthreads();
+    if (l < R && c0 + l < 1 + NALPHA) {
+      double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
+      for (int kk = 0; kk < N; ++kk) {
+        qc += part[l * N + kk][0];
+        vc += part[l * N + kk][1];
+        uc += part[l * N + kk][2];
+        cv += part[l * N + kk][3];
+      }
+      merit[c0 + l] = qc + vc + uc + P.mu * cv;
+    }
+    __syncthreads();
+    base = merit[0];
+    for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R && cc < 1 + NALPHA; ++cc) {
+      if (merit[cc] <= base) { found = cc; break; }
+    }
+    __syncthreads();
+  }
+  const double alpha = (found > 0) ? alphas[found - 1] : 0.0;
+  if (mode == 1) {
+    if (l == 0) alpha_out[b] = alpha;
+    return;
+  }
+  ProblemStats* st = stats + b;
+  if (alpha == 0.0) {
+    // src/osqp_sqp.py:81-82: `continue` re-solves the SAME QP from the same XU; the exact
+    // solve is deterministic, so every remaining iteration repeats alpha = 0.
+    if (l == 0) {
+      for (int it = iter; it < P.max_iters; ++it) st->alphas[st->n_alphas++] = 0.0;
+      st->qp_iters = P.max_iters;
+      active[b] = 0;
+    }
+    return;
+  }
+  double ss = 0.0;
+  for (int e = l; e < P.T; e += 64) {
+    const double stp = alpha * (S[e] - X[e]);
+    X[e] = X[e] + stp;
+    ss += stp * stp;
+  }
+  // wave reduction
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  if (l == 0) {
+    const double stepsize = sqrt(ss);
+    st->alphas[st->n_alphas++] = alpha;
+    st->stepsizes[st->n_steps++] = stepsize;
+    st->qp_iters = iter + 1;
+    if (stepsize < P.step_tol || iter + 1 >= P.max_iters) active[b] = 0;
+  }
+}
+
+// Merit pieces of a given XU (hooks for SQP_OSQP.eepos_cost / integrator_err).
+__global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, SolveParams P,
+                                              const double* __restrict__ xu, const double* __restrict__ xu_ref,
+                                              const double* __restrict__ goals, double* __restrict__ out) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  const int l = threadIdx.x;
+  const double* X = xu + (long)b * P.T;
+  __shared__ double part[MAXN][4];
+  for (int k = l; k < P.N; k += 64) {
+    double o[4];
+    merit_knot(*Mg, P, k, X + 18 * k, (k < P.N - 1) ? X + 18 * (k + 1) : X, goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride, o);
+    part[k][0] = o[0]; part[k][1] = o[1]; part[k][2] = o[2]; part[k][3] = o[3];
+  }
+  __syncthreads();
+  if (l == 0) {
+    double acc[4] = {0, 0, 0, 0};
+    for (int k = 0; k < P.N; ++k)
+      for (int j = 0; j < 4; ++j) acc[j] += part[k][j];
+    double dd = 0.0;
+    for (int i = 0; i < 12; ++i) {
+      const double t = X[i] - xu_ref[(long)b * P.T + i];
+      dd += t * t;
+    }
+    for (int j = 0; j < 4; ++j) out[b * 5 + j] = acc[j];
+    out[b * 5 + 4] = sqrt(dd);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Query kernels (one thread per query).
+__global__ void __launch_bounds__(256) k_eepos(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
+                                               double* __restrict__ p, double* __restrict__ J) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double c[6], s[6], pp[3], JJ[3][6];
+  sincos6(q + 6L * i, c, s);
+  fk_jac(*Mg, c, s, pp, JJ);
+  for (int r = 0; r < 3; ++r) p[3L * i + r] = pp[r];
+  if (J)
+    for (int r = 0; r < 3; ++r)
+      for (int j = 0; j < 6; ++j) J[18L * i + 6 * r + j] = JJ[r][j];
+}
+
+__global__ void __launch_bounds__(256) k_aba(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
+                                             const double* __restrict__ v, const double* __restrict__ tau,
+                                             const double* __restrict__ fext, double* __restrict__ a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double c[6], s[6], L[6][6], aa[6];
+  sincos6(q + 6L * i, c, s);
+  forward_dynamics(*Mg, c, s, v + 6L * i, tau + 6L * i, fext ? fext + 6L * i : nullptr, L, aa);
+  for (int r = 0; r < 6; ++r) a[6L * i + r] = aa[r];
+}
+
+// thread per (query, direction d<12)
+__global__ void __launch_bounds__(256) k_abad(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
+                                              const double* __restrict__ v, const double* __restrict__ tau,
+                                              double* __restrict__ dq, double* __restrict__ dv,
+                                              double* __restrict__ Minv, double* __restrict__ a) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(gid / 12), d = (int)(gid - 12L * (gid / 12));
+  if (i >= n) return;
+  double c[6], s[6], L[6][6], aa[6], col[6];
+  sincos6(q + 6L * i, c, s);
+  forward_dynamics(*Mg, c, s, v + 6L * i, tau + 6L * i, nullptr, L, aa);
+  aba_deriv_column(*Mg, c, s, v + 6L * i, aa, L, d, col);
+  if (d < 6) {
+    for (int r = 0; r < 6; ++r) dq[36L * i + 6 * r + d] = col[r];
+    double e[6] = {0, 0, 0, 0, 0, 0};
+    e[d] = 1.0;
+    chol6_solve(L, e);
+    for (int r = 0; r <= d; ++r) {
+      Minv[36L * i + 6 * r + d] = e[r];
+      Minv[36L * i + 6 * d + r] = e[r];
+    }
+    if (d == 0)
+      for (int r = 0; r < 6; ++r) a[6L * i + r] = aa[r];
+  } else {
+    for (int r = 0; r < 6; ++r) dv[36L * i + 6 * r + (d - 6)] = col[r];
+  }
+}
+
+// utils.rk4 (src/utils.py:3-18): 4 ABA evaluations, pin.integrate = q + v*dt.
+__global__ void __launch_bounds__(256) k_rk4(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
+                                             const double* __restrict__ v, const double* __restrict__ u, double dt,
+                                             const double* __restrict__ fext, double* __restrict__ qo,
+                                             double* __restrict__ vo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* f6 = fext ? fext + 6L * i : nullptr;
+  double q0[6], v0[6], uu[6], c[6], s[6], L[6][6];
+  for (int r = 0; r < 6; ++r) { q0[r] = q[6L * i + r]; v0[r] = v[6L * i + r]; uu[r] = u[6L * i + r]; }
+  double k1v[6], k2v[6], k3v[6], k4v[6], k2q[6], k3q[6], k4q[6], qq[6];
+  sincos6(q0, c, s);
+  forward_dynamics(*Mg, c, s, v0, uu, f6, L, k1v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + v0[r] * dt / 2; k2q[r] = v0[r] + k1v[r] * dt / 2; }
+  sincos6(qq, c, s);
+  forward_dynamics(*Mg, c, s, k2q, uu, f6, L, k2v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k2q[r] * dt / 2; k3q[r] = v0[r] + k2v[r] * dt / 2; }
+  sincos6(qq, c, s);
+  forward_dynamics(*Mg, c, s, k3q, uu, f6, L, k3v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k3q[r] * dt; k4q[r] = v0[r] + k3v[r] * dt; }
+  sincos6(qq, c, s);
+  forward_dynamics(*Mg, c, s, k4q, uu, f6, L, k4v);
+  for (int r = 0; r < 6; ++r) {
+    vo[6L * i + r] = v0[r] + (dt / 6) * (k1v[r] + 2 * k2v[r] + 2 * k3v[r] + k4v[r]);
+    const double avg = (v0[r] + 2 * k2q[r] + 2 * k3q[r] + k4q[r]) / 6;
+    qo[6L * i + r] = q0[r] + avg * dt;
+  }
+}
+
+}  // namespace i7m

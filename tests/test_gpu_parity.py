@@ -1,0 +1,103 @@
+"""GPU parity: every kernel on the hot path against the CPU oracle, through the C-ABI.
+
+Tolerances (fp64 throughout; the reference computes in fp64):
+  kinematics / dynamics / derivatives : 1e-10 relative (rounding-order differences only)
+  QP solution vs exact sparse-LU KKT  : 1e-8 relative (SURVEY.md §8d parity gate)
+  full SQP trajectory                 : 1e-6 relative per problem, with the line-search
+                                        alpha sequence identical (ties are measure-zero)
+"""
+import numpy as np
+import pytest
+
+from oracle import rbd
+from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def _handle(lib, model, N, B):
+    return lib.Handle(model, N=N, max_batch=B)
+
+
+def test_eepos_kats_and_jacobian(lib, model):
+    h = _handle(lib, model, 16, 4)
+    rng = np.random.default_rng(1)
+    q = rng.uniform(-3, 3, size=(257, 6))
+    p, J = h.eepos(q, jacobian=True)
+    for i in range(0, 257, 16):
+        pe, Je = rbd.d_eepos(q[i])
+        np.testing.assert_allclose(p[i], pe, rtol=0, atol=1e-13)
+        np.testing.assert_allclose(J[i], Je, rtol=0, atol=1e-13)
+    kat = h.eepos(0.3 * np.ones(6))[0]
+    np.testing.assert_allclose(kat, [-0.34013996, -0.30723899, 1.15448739], atol=5e-9)
+
+
+def test_aba_and_derivatives(lib, model):
+    h = _handle(lib, model, 16, 4)
+    rng = np.random.default_rng(2)
+    n = 64
+    q, v, t = rng.uniform(-3, 3, (n, 6)), rng.uniform(-2, 2, (n, 6)), rng.uniform(-50, 50, (n, 6))
+    a = h.aba(q, v, t)
+    dq, dv, Mi, a2 = h.aba_derivatives(q, v, t)
+    for i in range(0, n, 7):
+        ra = rbd.aba(q[i], v[i], t[i])
+        np.testing.assert_allclose(a[i], ra, rtol=1e-10, atol=1e-9)
+        np.testing.assert_allclose(a2[i], ra, rtol=1e-10, atol=1e-9)
+        rdq, rdv, rMi, _ = rbd.aba_derivatives(q[i], v[i], t[i])
+        for got, ref in ((dq[i], rdq), (dv[i], rdv), (Mi[i], rMi)):
+            assert np.abs(got - ref).max() <= 1e-10 * max(1.0, np.abs(ref).max())
+        assert np.array_equal(Mi[i], Mi[i].T)
+
+
+def test_rk4_with_fext(lib, model):
+    h = _handle(lib, model, 16, 4)
+    rng = np.random.default_rng(3)
+    n = 16
+    q, v, u = rng.uniform(-3, 3, (n, 6)), rng.uniform(-1, 1, (n, 6)), rng.uniform(-20, 20, (n, 6))
+    f = rng.normal(0, 10, (n, 6))
+    qo, vo = h.rk4(q, v, u, 0.01, fext=f)
+    for i in range(n):
+        fext = [np.zeros(6)] * 5 + [f[i]]
+        rq, rv = rbd.rk4(q[i], v[i], u[i], 0.01, fext=fext)
+        np.testing.assert_allclose(qo[i], rq, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(vo[i], rv, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_qp_matches_exact_kkt(lib, model, N):
+    B = 3
+    xcur, goals, XU = synthetic_batch(B, N, seed=7)
+    # a non-trivial linearisation point: perturb the trajectory
+    XU = XU + np.random.default_rng(0).normal(0, 0.3, XU.shape)
+    h = _handle(lib, model, N, B)
+    sol = h.qp(XU, xcur, goals)
+    for b in range(B):
+        s = OSQPSolverRef(N=N)
+        ref = s.setup_and_solve_qp(XU[b], xcur[b], goals[b]).x
+        rel = np.linalg.norm(sol[b] - ref) / np.linalg.norm(ref)
+        assert rel < 1e-8, rel
+
+
+@pytest.mark.parametrize("N,B", [(16, 6), (32, 4)])
+def test_full_sqp_matches_oracle(lib, model, N, B):
+    xcur, goals, XU = synthetic_batch(B, N, seed=42 + N)
+    h = _handle(lib, model, N, B)
+    out, st = h.solve(xcur, goals, XU)
+    for b in range(B):
+        sq = SQPRef(OSQPSolverRef(N=N))
+        ref = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        s = sq.get_stats()
+        assert st["qp_iters"][b] == s["qp_iters"]["values"][0]
+        na = st["n_alphas"][b]
+        np.testing.assert_array_equal(st["alphas"][b][:na], s["linesearch_alphas"]["values"])
+        rel = np.linalg.norm(out[b] - ref) / np.linalg.norm(ref)
+        assert rel < 1e-6, (b, rel)
