@@ -25,6 +25,7 @@
  *   i7m_aba                    pin.aba (+f_ext)               src/osqp_sqp.py:40, src/utils.py:5
  *   i7m_aba_derivatives        pin.computeABADerivatives      src/osqp_solver.py:71,76
  *   i7m_rk4                    utils.rk4 (plant)              src/utils.py:3-18
+ *   i7m_set_external_wrench    batch_sqp.set_external_wrench_batch  gato_controller.py:129
  *
  * Layouts (all fp64, C-contiguous, row = problem):
  *   XU    (B, T)  T = 18N-6, [x_0,u_0,x_1,u_1,...,x_{N-1}], x=[q(6),v(6)]  src/osqp_solver.py:22
@@ -108,6 +109,11 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out);
 void i7m_destroy(i7m_handle* h);
 int i7m_set_stream(i7m_handle* h, void* stream);  /* NULL -> the handle's own stream */
 int i7m_synchronize(i7m_handle* h);
+/* Constant external wrench [force; torque] on joint 6, in its LOCAL frame (pinocchio f_ext
+ * convention, src/gato_mpc_batch_sample.py:151-161), one per problem, used by every
+ * dynamics evaluation of subsequent solves (linearisation and merit).  fext (B, 6);
+ * NULL clears it.  Backs batch_sqp.set_external_wrench_batch (gato_controller.py:129). */
+int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext);
 
 /* Full SQP solve, host buffers in/out (H2D + kernels + D2H, synchronous). */
 int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,

@@ -97,6 +97,7 @@ SIGNATURES = [
     ("i7m_destroy", None, [_H]),
     ("i7m_set_stream", C.c_int, [_H, C.c_void_p]),
     ("i7m_synchronize", C.c_int, [_H]),
+    ("i7m_set_external_wrench", C.c_int, [_H, C.c_int32, _DP]),
     ("i7m_solve", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP, C.c_void_p]),
     ("i7m_solve_device", C.c_int, [_H, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                    C.c_void_p]),
@@ -297,6 +298,14 @@ class Handle:
     # ---- timing --------------------------------------------------------------------------
     def set_stream(self, stream_ptr: int):
         _check(self._lib.i7m_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def set_external_wrench(self, fext):
+        """(B, 6) local joint-6 wrench per problem, or None to clear."""
+        if fext is None:
+            _check(self._lib.i7m_set_external_wrench(self._h, 0, None))
+            return
+        f = _f64(fext).reshape(-1, 6)
+        _check(self._lib.i7m_set_external_wrench(self._h, f.shape[0], _ptr(f)))
 
     def synchronize(self):
         _check(self._lib.i7m_synchronize(self._h))

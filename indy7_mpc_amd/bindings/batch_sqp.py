@@ -1,0 +1,119 @@
+"""Drop-in for the ``bindings.batch_sqp`` module the reference's GATO controllers import
+(gato_controller.py:53-68,95,106,129,132-138; src/gato_mpc_batch.py:12-29,43).
+
+The reference binding is an external CUDA module (absent).  This one keeps its
+Python surface — ``SQPSolverfloat_{1..256}`` with ``solve``, ``reset``, ``resetRho``,
+``resetLambda``, ``set_external_wrench_batch`` and ``sim_forward`` — and solves the OSQP
+formulation of src/osqp_solver.py (fp64, exact QP) on the GPU.  N is taken from the XU width
+(traj_len = 18N - 6); goals use the GATO layout (B, 6N), first 3 of every 6 used.
+
+External wrench convention: [force; torque] on joint 6 in its LOCAL frame (pinocchio's f_ext,
+as src/gato_mpc_batch_sample.py:151-161 builds it); ``world_to_local_wrench`` converts a
+world-frame wrench at a given configuration the same way the reference's host code does.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from .. import _lib
+from ..model import default_model
+
+_SIZES = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+
+
+class _SQPSolverBatch:
+    batch_size = 1
+
+    def __init__(self, model=None, device_id=0):
+        self.model = model or default_model()
+        self.device_id = device_id
+        self._h = None
+        self._key = None
+        self._fext = np.zeros((self.batch_size, 6))
+        self._sim = _lib.Handle(self.model, N=2, max_batch=max(self.batch_size, 1), device_id=device_id)
+
+    def _handle(self, N, dt):
+        if self._key != (N, dt):
+            self._h = _lib.Handle(self.model, N=N, dt=dt, max_batch=self.batch_size, device_id=self.device_id)
+            self._key = (N, dt)
+            if np.any(self._fext):
+                self._h.set_external_wrench(self._fext)
+        return self._h
+
+    def solve(self, XU_batch, dt, xcur_batch, eepos_goals_batch):
+        XU = np.asarray(XU_batch, dtype=float).reshape(self.batch_size, -1)
+        T = XU.shape[1]
+        if (T + 6) % 18:
+            raise ValueError(f"XU width {T} is not 18N-6")
+        N = (T + 6) // 18
+        h = self._handle(N, float(dt))
+        t0 = time.perf_counter()
+        out, st = h.solve(np.asarray(xcur_batch, float).reshape(self.batch_size, 12),
+                          np.asarray(eepos_goals_batch, float).reshape(self.batch_size, -1), XU)
+        t1 = time.perf_counter()
+        iters = int(st["qp_iters"].max()) if len(st) else 0
+        ls = []
+        for it in range(iters):
+            ls.append({"step_size": np.array([s["alphas"][it] if it < s["n_alphas"] else 0.0 for s in st])})
+        return {
+            "xu_trajectory": out,
+            "solve_time_us": (t1 - t0) * 1e6,
+            "sqp_iterations": st["qp_iters"].copy(),
+            "pcg_stats": [{"pcg_iterations": 0} for _ in range(iters)],  # exact KKT solve, no PCG
+            "line_search_stats": ls,
+        }
+
+    def reset(self):
+        """Warm-start state reset; the exact solve keeps no solver state between calls."""
+
+    def resetRho(self):
+        """ADMM/PCG penalty reset; a no-op for the exact solve."""
+
+    def resetLambda(self):
+        """Dual reset; a no-op for the exact solve."""
+
+    def set_external_wrench_batch(self, f_ext_batch):
+        f = np.asarray(f_ext_batch, dtype=float).reshape(self.batch_size, 6)
+        self._fext = f.copy()
+        if self._h is not None:
+            self._h.set_external_wrench(self._fext)
+
+    def sim_forward(self, x, u, dt):
+        """One rk4 step of x (12,) under u (6,) for every wrench hypothesis -> (B, 12)."""
+        x = np.asarray(x, float).reshape(12)
+        u = np.asarray(u, float).reshape(6)
+        B = self.batch_size
+        qo, vo = self._sim.rk4(np.tile(x[:6], (B, 1)), np.tile(x[6:], (B, 1)), np.tile(u, (B, 1)), float(dt),
+                               fext=self._fext)
+        return np.hstack([qo, vo])
+
+
+def world_to_local_wrench(model, q, f_world):
+    """World-frame wrench [f; n] at the joint-6 origin's world placement -> local frame
+    (pinocchio ``oMi[6].actInv(Force)``, src/gato_mpc_batch_sample.py:151-161)."""
+    from ..utils import query_handle
+
+    q = np.asarray(q, float).reshape(6)
+    p, _ = query_handle(model).eepos(q, jacobian=True)
+    R = _rotation_joint6(model, q)
+    f = np.asarray(f_world, float).reshape(6)
+    fl = R.T @ f[:3]
+    nl = R.T @ (f[3:] - np.cross(p[0], f[:3]))
+    return np.concatenate([fl, nl])
+
+
+def _rotation_joint6(model, q):
+    R = np.eye(3)
+    for i in range(6):
+        c, s = np.cos(q[i]), np.sin(q[i])
+        Rz = np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
+        R = R @ np.asarray(model.params["placement_R"][i]) @ Rz
+    return R
+
+
+for _n in _SIZES:
+    globals()[f"SQPSolverfloat_{_n}"] = type(f"SQPSolverfloat_{_n}", (_SQPSolverBatch,), {"batch_size": _n})
+
+__all__ = [f"SQPSolverfloat_{n}" for n in _SIZES] + ["world_to_local_wrench"]

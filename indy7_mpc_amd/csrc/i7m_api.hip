@@ -53,6 +53,8 @@ struct i7m_handle {
          *d_cost = nullptr, *d_kbuf = nullptr, *d_aux = nullptr, *d_out = nullptr;
   int* d_active = nullptr;
   ProblemStats* d_stats = nullptr;
+  double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
+  bool has_fext = false;
   size_t goal_cap = 0;
   // timing
   bool timing = false;
@@ -153,8 +155,8 @@ int launch_linearize(i7m_handle* h, const SolveParams& P, const double* xu, cons
   const int blk = 256;
   const int grid = (int)((nthr + blk - 1) / blk);
   return timed(h, I7M_K_LIN, [&] {
-    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(blk), 0, h->stream, h->d_model, P, xu, goals, active, h->d_lin,
-                       h->d_cost);
+    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(blk), 0, h->stream, h->d_model, P, xu, goals,
+                       h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
   });
 }
 
@@ -171,8 +173,8 @@ int launch_linesearch(i7m_handle* h, const SolveParams& P, double* xu, const dou
                       int* active, ProblemStats* st, double* alpha_out, int iter, int mode) {
   if (P.B == 0) return I7M_OK;
   return timed(h, I7M_K_LINESEARCH, [&] {
-    hipLaunchKernelGGL(k_linesearch, dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals, active, st,
-                       alpha_out, iter, mode);
+    hipLaunchKernelGGL(k_linesearch, dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
+                       h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
   });
 }
 
@@ -280,7 +282,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_cost, Bm * N * COST_STRIDE * 8) &&
             alloc((void**)&h->d_kbuf, Bm * (N - 1) * KBUF_STRIDE * 8) && alloc((void**)&h->d_aux, scratch * 8) &&
             alloc((void**)&h->d_out, scratch * 8) &&
-            alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats));
+            alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
+            alloc((void**)&h->d_fext, Bm * 6 * 8);
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
   DevModel dm = make_dev_model(cfg->model);
   if (hipMemcpy(h->d_model, &dm, sizeof(dm), hipMemcpyHostToDevice) != hipSuccess)
@@ -294,7 +297,7 @@ void i7m_destroy(i7m_handle* h) {
   hipSetDevice(h->dev);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats};
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& t : h->ev) {
@@ -309,6 +312,21 @@ void i7m_destroy(i7m_handle* h) {
 int i7m_set_stream(i7m_handle* h, void* stream) {
   if (!h) return fail(I7M_EINVAL, "null handle");
   h->stream = stream ? (hipStream_t)stream : h->own;
+  return I7M_OK;
+}
+
+int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (!fext) {
+    h->has_fext = false;
+    return I7M_OK;
+  }
+  if (B < 1 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "external wrench batch outside [1, max_batch]");
+  HIPCHK(hipSetDevice(h->dev));
+  HIPCHK(hipMemsetAsync(h->d_fext, 0, (size_t)h->cfg.max_batch * 6 * 8, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d_fext, fext, (size_t)B * 6 * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->has_fext = true;
   return I7M_OK;
 }
 
@@ -400,7 +418,8 @@ int i7m_merit(i7m_handle* h, int32_t B, const double* xu, const double* xu_ref, 
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_aux, xu_ref, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  hipLaunchKernelGGL(k_merit, dim3(B), dim3(64), 0, h->stream, h->d_model, P, h->d_xu, h->d_aux, h->d_goal, h->d_out);
+  hipLaunchKernelGGL(k_merit, dim3(B), dim3(64), 0, h->stream, h->d_model, P, h->d_xu, h->d_aux, h->d_goal,
+                     h->has_fext ? h->d_fext : nullptr, h->d_out);
   HIPCHK(hipGetLastError());
   if ((rc = copy_out(h, out, h->d_out, (size_t)B * 5))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));

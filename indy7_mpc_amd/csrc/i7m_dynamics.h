@@ -316,7 +316,7 @@ __device__ __forceinline__ void forward_dynamics(const DevModel& Md, const doubl
 // out = -M^-1 dRNEA/dx_d (a held fixed).
 __device__ __forceinline__ void aba_deriv_column(const DevModel& Md, const double c[6], const double s[6],
                                                  const double v[6], const double a[6], const double L[6][6],
-                                                 int d, double out[6]) {
+                                                 int d, const double* fext6, double out[6]) {
   dual dc[6], ds[6], dv[6], da[6], dt[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -326,7 +326,7 @@ __device__ __forceinline__ void aba_deriv_column(const DevModel& Md, const doubl
     dv[i] = dual{v[i], (d - 6 == i) ? 1.0 : 0.0};
     da[i] = dual{a[i], 0.0};
   }
-  rnea<dual>(Md, dc, ds, dv, da, true, nullptr, dt);
+  rnea<dual>(Md, dc, ds, dv, da, true, fext6, dt);
 #pragma unroll
   for (int i = 0; i < 6; ++i) out[i] = -dt[i].d;
   chol6_solve(L, out);

@@ -63,8 +63,8 @@ __device__ __forceinline__ void cost_knot(const DevModel& Md, const SolveParams&
 
 __global__ void __launch_bounds__(256) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
                                                    const double* __restrict__ xu, const double* __restrict__ goals,
-                                                   const int* __restrict__ active, double* __restrict__ lin,
-                                                   double* __restrict__ cost) {
+                                                   const double* __restrict__ fext, const int* __restrict__ active,
+                                                   double* __restrict__ lin, double* __restrict__ cost) {
   const int per = 12 * (P.N - 1);
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int b = (int)(gid / per);
@@ -80,9 +80,10 @@ __global__ void __launch_bounds__(256) k_linearize(const DevModel* __restrict__ 
   for (int i = 0; i < 6; ++i) { q[i] = X[i]; v[i] = X[6 + i]; u[i] = X[12 + i]; }
   double c[6], s[6], L[6][6], a[6];
   sincos6(q, c, s);
-  forward_dynamics(Md, c, s, v, u, nullptr, L, a);
+  const double* f6 = fext ? fext + 6L * b : nullptr;
+  forward_dynamics(Md, c, s, v, u, f6, L, a);
   double col[6];
-  aba_deriv_column(Md, c, s, v, a, L, d, col);
+  aba_deriv_column(Md, c, s, v, a, L, d, f6, col);
   double* out = lin + ((long)b * (P.N - 1) + k) * LIN_STRIDE;
   const double dt = P.dt;
   if (d < 6) {
@@ -364,7 +365,7 @@ __global__ void __launch_bounds__(64) k_riccati(SolveParams P, const double* __r
 // Merit pieces of one knot (src/osqp_sqp.py:13-47): qcost, vcost, ucost, integrator error.
 // x: 18 values of knot k (12 at the last knot), xn: the 12 state values of knot k+1.
 __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams& P, int k, const double* x,
-                                           const double* xn, const double* goal, double out[4]) {
+                                           const double* xn, const double* goal, const double* f6, double out[4]) {
   double c[6], s[6], p[3];
   sincos6(x, c, s);
   fk_jac(Md, c, s, p, nullptr);
@@ -383,7 +384,7 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
     for (int i = 0; i < 6; ++i) uu += x[12 + i] * x[12 + i];
     out[2] = P.R * uu;
     double L[6][6], a[6];
-    forward_dynamics(Md, c, s, x + 6, x + 12, nullptr, L, a);
+    forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
     double eq = 0.0, ev = 0.0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
@@ -402,7 +403,8 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha.
 __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    double* __restrict__ xu, const double* __restrict__ sol,
-                                                   const double* __restrict__ goals, int* __restrict__ active,
+                                                   const double* __restrict__ goals, const double* __restrict__ fext,
+                                                   int* __restrict__ active,
                                                    ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
                                                    int iter, int mode) {
   const int b = blockIdx.x;
@@ -418,9 +420,7 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   const double* S = sol + (long)b * P.T;
   __shared__ double part[64][4];
   __shared__ double merit[9];
-  __shared__ int chosen;
   const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
-  if (l == 0) chosen = -1;
   double base = 0.0;
   int found = -1;
   for (int c0 = 0; c0 < 1 + NALPHA && found < 0; c0 += R) {
@@ -439,7 +439,8 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
           for (int i = 0; i < 12; ++i) xn[i] = X[18 * (k + 1) + i] + al * (S[18 * (k + 1) + i] - X[18 * (k + 1) + i]);
       }
       double o[4];
-      merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride, o);
+      merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride,
+                 fext ? fext + 6L * b : nullptr, o);
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
         double dd = 0.0;
@@ -506,7 +507,8 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
 // Merit pieces of a given XU (hooks for SQP_OSQP.eepos_cost / integrator_err).
 __global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, SolveParams P,
                                               const double* __restrict__ xu, const double* __restrict__ xu_ref,
-                                              const double* __restrict__ goals, double* __restrict__ out) {
+                                              const double* __restrict__ goals, const double* __restrict__ fext,
+                                              double* __restrict__ out) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
   const int l = threadIdx.x;
@@ -514,7 +516,8 @@ __global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, S
   __shared__ double part[MAXN][4];
   for (int k = l; k < P.N; k += 64) {
     double o[4];
-    merit_knot(*Mg, P, k, X + 18 * k, (k < P.N - 1) ? X + 18 * (k + 1) : X, goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride, o);
+    merit_knot(*Mg, P, k, X + 18 * k, (k < P.N - 1) ? X + 18 * (k + 1) : X, goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride,
+               fext ? fext + 6L * b : nullptr, o);
     part[k][0] = o[0]; part[k][1] = o[1]; part[k][2] = o[2]; part[k][3] = o[3];
   }
   __syncthreads();
@@ -569,7 +572,7 @@ __global__ void __launch_bounds__(256) k_abad(const DevModel* __restrict__ Mg, i
   double c[6], s[6], L[6][6], aa[6], col[6];
   sincos6(q + 6L * i, c, s);
   forward_dynamics(*Mg, c, s, v + 6L * i, tau + 6L * i, nullptr, L, aa);
-  aba_deriv_column(*Mg, c, s, v + 6L * i, aa, L, d, col);
+  aba_deriv_column(*Mg, c, s, v + 6L * i, aa, L, d, nullptr, col);
   if (d < 6) {
     for (int r = 0; r < 6; ++r) dq[36L * i + 6 * r + d] = col[r];
     double e[6] = {0, 0, 0, 0, 0, 0};

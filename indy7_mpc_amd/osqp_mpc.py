@@ -1,0 +1,67 @@
+"""Drop-in for reference ``MPC_OSQP`` (src/osqp_mpc.py:5-72): the closed-loop driver.
+
+Each MPC step is one GPU SQP solve (SQP_OSQP.sqp) plus the GPU rk4 plant step.  The
+reference's quirks are kept on purpose: the plant is driven with the PREVIOUS trajectory's
+first control (``XU``, not ``xu_new``, :56), the warm start is shifted by the number of full
+dt steps simulated (:64-65), and the first/last states are pinned to xcur and
+[1,...,1, 0,...,0] (:68-70).  The reference's rk4 call passes no f_ext (:56); the external
+force is zero here as in the notebook run (notebooks/pin_mpc_indy7.ipynb cell 2).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .utils import rk4
+
+
+class MPC_OSQP:
+    def __init__(self, model, sqp_optimizer, solver):
+        self.model = model
+        self.model.gravity.linear = np.array([0, 0, -9.81])  # reference :8-9
+        self.sqp_optimizer = sqp_optimizer
+        self.solver = solver
+        self.xpath = []
+        self.goal_distances = []
+
+    def run_mpc(self, xstart, endpoints, num_steps=500, verbose=True):
+        nq, nv, nx, nu = self.solver.nq, self.solver.nv, self.solver.nx, self.solver.nu
+        xcur = np.asarray(xstart, dtype=float)
+        endpoint_ind = 0
+        endpoint = endpoints[endpoint_ind]
+        eepos_goal = np.tile(endpoint, self.solver.N).T
+        XU = np.zeros(self.solver.N * (nx + nu) - nu)
+        XU = self.sqp_optimizer.sqp(xcur, eepos_goal, XU)
+        for i in range(num_steps):
+            cur_eepos = self.solver.eepos(xcur[:nq])
+            goaldist = np.linalg.norm(cur_eepos - eepos_goal[:3])
+            if goaldist < 1e-1:
+                if verbose:
+                    print("switching goals")
+                endpoint_ind = (endpoint_ind + 1) % len(endpoints)
+                endpoint = endpoints[endpoint_ind]
+                eepos_goal = np.tile(endpoint, self.solver.N).T
+            if verbose:
+                print(goaldist)
+            self.goal_distances.append(goaldist)
+            if goaldist > 1.1:
+                if verbose:
+                    print("breaking on big goal dist")
+                break
+            xu_new = self.sqp_optimizer.sqp(xcur, eepos_goal, XU)
+            trajopt_time = 0.01
+            sim_time = trajopt_time
+            sim_steps = 0
+            while sim_time > 0:
+                timestep = min(sim_time, self.solver.dt)
+                control = XU[sim_steps * (nx + nu) + nx:(sim_steps + 1) * (nx + nu)]
+                qn, vn = rk4(self.model, self.solver.data, xcur[:nq], xcur[nq:nx], control, timestep)
+                xcur = np.concatenate([qn, vn])
+                if timestep > 0.5 * self.solver.dt:
+                    sim_steps += 1
+                sim_time -= timestep
+                self.xpath.append(xcur[:nq])
+            if sim_steps > 0:
+                XU[:-(sim_steps) * (nx + nu) or len(XU)] = xu_new[(sim_steps) * (nx + nu):]
+            XU[:nx] = xcur.reshape(-1)
+            XU[-nx:] = np.hstack([np.ones(nq), np.zeros(nv)])
+        return self.xpath

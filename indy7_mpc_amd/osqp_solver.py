@@ -1,0 +1,177 @@
+"""Drop-in for reference ``OSQPSolver`` (src/osqp_solver.py:6-155).
+
+Same constructor, attributes and methods.  The numbers come from the GPU:
+  * ``setup_and_solve_qp`` linearises on the device (k_linearize) and solves the QP EXACTLY
+    with the block-tridiagonal Riccati kernel (k_riccati).  The reference hands the same
+    P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.
+  * ``Pdata/Adata/l/g`` (the CSC value arrays the reference fills, :95-135) are assembled on
+    the host from the device linearisation, in the reference's exact value order, only when
+    ``update_constraint_matrix`` / ``update_cost_matrix`` are called (they are not needed by
+    the solve itself).
+  * ``eepos`` / ``d_eepos`` are device FK / Jacobian queries.
+Extra (not in the reference): ``max_batch`` / ``device_id`` kwargs size the device buffers
+for the batched entry point ``SQP_OSQP.sqp_batch``.
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.sparse import bmat, csc_matrix, triu
+
+from . import _lib
+
+
+class QPSolution:
+    """What ``osqp.OSQP().solve()`` returns, as far as the reference uses it (``.x``)."""
+
+    def __init__(self, x, status="solved"):
+        self.x = x
+        self.y = None
+        self.info = type("info", (), {"status": status, "iter": 0})()
+
+
+class OSQPSolver:
+    def __init__(self, model, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
+                 max_batch=1, device_id=0):
+        self.model = model
+        self.data = model.createData()
+        self.N = N
+        self.dt = dt
+        self.nq = model.nq
+        self.nv = model.nv
+        self.nx = self.nq + self.nv
+        self.nu = len(model.joints) - 1
+        self.nxu = self.nx + self.nu
+        self.traj_len = (self.nx + self.nu) * self.N - self.nu
+        self.dQ_cost = dQ_cost
+        self.R_cost = R_cost
+        self.QN_cost = QN_cost
+        self.regularize = regularize
+        self.eps = eps
+        self.A = self.initialize_A()
+        self.l = np.zeros(self.N * self.nx)
+        self.P = self.initialize_P()
+        self.g = np.zeros(self.traj_len)
+        self.Pdata = np.zeros(self.P.nnz)
+        self.Adata = np.zeros(self.A.nnz)
+        self.A_k = np.vstack([-1.0 * np.eye(self.nx),
+                              np.vstack([np.hstack([np.eye(self.nq), self.dt * np.eye(self.nq)]),
+                                         np.ones((self.nq, 2 * self.nq))])])
+        self.B_k = np.zeros((self.nx, self.nq))
+        self.cx_k = np.zeros(self.nx)
+        self.handle = _lib.Handle(model, N=N, dt=dt, dQ_cost=dQ_cost, R_cost=R_cost, QN_cost=QN_cost,
+                                  regularize=regularize, eps=eps, max_batch=max_batch, device_id=device_id)
+
+    # ---- sparsity templates (src/osqp_solver.py:48-68) -----------------------------------
+    def initialize_P(self):
+        block = np.eye(self.nxu)
+        block[: self.nq, : self.nq] = np.ones((self.nq, self.nq))
+        bd = np.kron(np.eye(self.N), block)[: -self.nu, : -self.nu]
+        return csc_matrix(triu(bd), shape=(self.traj_len, self.traj_len))
+
+    def initialize_A(self):
+        nx, nu, N = self.nx, self.nu, self.N
+        blocks = [[np.ones((nx, nx))] + [None] * (2 * N)]
+        for i in range(N - 1):
+            row = [None] * (2 * i) + [np.ones((nx, nx)), 2 * np.ones((nx, nu)), -1 * np.ones((nx, nx))]
+            row += [None] * (2 * N + 1 - len(row))
+            blocks.append(row)
+        return bmat(blocks, format="csc")
+
+    # ---- linearisation (src/osqp_solver.py:70-135), values from the device --------------
+    def compute_dynamics_jacobians(self, q, v, u):
+        dq, dv, Minv, a = self.handle.aba_derivatives(q, v, u)
+        nx, nq = self.nx, self.nq
+        self.A_k[nx + nq:, :nq] = dq[0] * self.dt
+        self.A_k[nx + nq:, nq:2 * nq] = dv[0] * self.dt + np.eye(self.nv)
+        self.B_k[nq:, :] = Minv[0] * self.dt
+        xnext = np.hstack([q + v * self.dt, v + a[0] * self.dt])
+        self.cx_k = xnext - self.A_k[nx:] @ np.hstack([q, v]) - self.B_k @ u
+
+    def _linearisation(self, xu, eepos_g):
+        lin, cost = self.handle.linearize(xu, eepos_g)
+        return lin[0], cost[0]
+
+    def update_constraint_matrix(self, xu, xs, _lin=None):
+        lin = self._linearisation(xu, np.zeros(3 * self.N))[0] if _lin is None else _lin
+        self.Adata[:], self.l[:] = assemble_A(lin, np.asarray(xu, float), np.asarray(xs, float), self.dt, self.N)
+
+    def update_cost_matrix(self, XU, eepos_g, _cost=None):
+        cost = self._linearisation(XU, eepos_g)[1] if _cost is None else _cost
+        self.Pdata[:], self.g[:] = assemble_P(cost, np.asarray(XU, float), self.N)
+
+    def setup_and_solve_qp(self, xu, xs, eepos_g):
+        """reference :137-143 — linearise at xu, solve the QP; returns an object with ``.x``."""
+        return QPSolution(self.handle.qp(xu, xs, eepos_g)[0])
+
+    def assemble(self, xu, xs, eepos_g):
+        """Fill Pdata/Adata/l/g exactly as the reference's update_* methods do."""
+        lin, cost = self._linearisation(xu, eepos_g)
+        self.update_constraint_matrix(xu, xs, _lin=lin)
+        self.update_cost_matrix(xu, eepos_g, _cost=cost)
+
+    # ---- end effector (src/osqp_solver.py:146-155) -------------------------------------
+    def eepos(self, q):
+        return self.handle.eepos(q)[0]
+
+    def d_eepos(self, q):
+        p, J = self.handle.eepos(q, jacobian=True)
+        return p[0], J[0]
+
+
+def assemble_A(lin, xu, xs, dt, N):
+    """CSC values of A and l in the order of src/osqp_solver.py:83-101, from the device
+    linearisation lin (N-1, 114) = Aq | Av | Bu | a per knot."""
+    nx = 12
+    Adata = np.empty(360 * (N - 1) + 144)
+    l = np.empty(N * nx)
+    l[:nx] = -xs
+    Ak = np.zeros((24, 12))
+    Ak[:12] = -np.eye(12)
+    Ak[12:18, :6] = np.eye(6)
+    Ak[12:18, 6:] = dt * np.eye(6)
+    Bk = np.zeros((12, 6))
+    ind = 0
+    for k in range(N - 1):
+        Aq = lin[k, 0:36].reshape(6, 6)
+        Av = lin[k, 36:72].reshape(6, 6)
+        Bu = lin[k, 72:108].reshape(6, 6)
+        a = lin[k, 108:114]
+        Ak[18:, :6] = Aq
+        Ak[18:, 6:] = Av
+        Bk[6:] = Bu
+        Adata[ind:ind + 288] = Ak.T.reshape(-1)
+        ind += 288
+        Adata[ind:ind + 72] = Bk.T.reshape(-1)
+        ind += 72
+        x = xu[18 * k:18 * k + 12]
+        u = xu[18 * k + 12:18 * k + 18]
+        xnext = np.hstack([x[:6] + x[6:] * dt, x[6:] + a * dt])
+        c = xnext - Ak[12:] @ x - Bk @ u
+        l[(k + 1) * nx:(k + 2) * nx] = -c
+    Adata[ind:] = -np.eye(nx).reshape(-1)
+    return Adata, l
+
+
+def assemble_P(cost, xu, N):
+    """CSC values of P (upper) and g in the order of src/osqp_solver.py:103-135, from the device
+    cost linearisation cost (N, 10) = j(6) | Qm | dQm | Rm | |e|."""
+    Pdata = np.empty(27 * N + 6 * (N - 1))
+    g = np.empty(18 * N - 6)
+    tri = np.tril_indices(6)
+    ind = 0
+    for k in range(N):
+        j = cost[k, :6]
+        Qm, dQm, Rm = cost[k, 6], cost[k, 7], cost[k, 8]
+        g0 = 18 * k
+        g[g0:g0 + 6] = Qm * j
+        g[g0 + 6:g0 + 12] = dQm * xu[g0 + 6:g0 + 12]
+        ph = np.outer(j, j)
+        Pdata[ind:ind + 21] = Qm * ph[tri]
+        ind += 21
+        Pdata[ind:ind + 6] = dQm
+        ind += 6
+        if k < N - 1:
+            Pdata[ind:ind + 6] = Rm
+            ind += 6
+            g[g0 + 12:g0 + 18] = Rm * xu[g0 + 12:g0 + 18]
+    return Pdata, g

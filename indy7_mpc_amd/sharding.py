@@ -1,0 +1,64 @@
+"""Batch sharding across GPUs: problems are independent, so a batch of B
+problems splits into contiguous row ranges, one per device, with no collective.
+
+Two launch styles:
+  * one process per GPU (torch.distributed.run; bench.py): each rank takes
+    ``shard_range(B, rank, world)`` of the global batch;
+  * one process, many GPUs: :class:`ShardedSQP` runs one host thread per device (ctypes drops
+    the GIL inside the library call, so the devices work concurrently) and concatenates.
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+def shard_range(B: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) of a B-row batch owned by ``rank`` of ``world`` (sizes differ by <= 1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, rem = divmod(B, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def shard_ranges(B: int, world: int) -> List[Tuple[int, int]]:
+    return [shard_range(B, r, world) for r in range(world)]
+
+
+class ShardedSQP:
+    """Full SQP solves of a (B, .) batch split over several GPUs of this process."""
+
+    def __init__(self, model, devices: Sequence[int], N=32, max_batch_per_device=4096, **cost_kw):
+        from . import _lib
+
+        self.devices = list(devices)
+        self.handles = [_lib.Handle(model, N=N, max_batch=max_batch_per_device, device_id=d, **cost_kw)
+                        for d in self.devices]
+        self.N = N
+
+    def solve(self, xcur, goals, XU):
+        XU = np.ascontiguousarray(XU, dtype=float)
+        B = XU.shape[0]
+        ranges = shard_ranges(B, len(self.handles))
+        outs = [None] * len(self.handles)
+        errs = []
+
+        def work(i, lo, hi):
+            try:
+                if hi > lo:
+                    outs[i] = self.handles[i].solve(xcur[lo:hi], goals[lo:hi], XU[lo:hi])
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(i, lo, hi)) for i, (lo, hi) in enumerate(ranges)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        parts = [o for o in outs if o is not None]
+        return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
