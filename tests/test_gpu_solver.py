@@ -1,0 +1,255 @@
+"""GPU: the drop-in surfaces and the batched solver against the committed golden fixtures,
+the reference notebooks' printed outputs, and size-independent properties at bench scale.
+
+Tolerances (fp64):
+  golden linearisation (CSC values)        1e-10 relative to the array's max
+  golden exact QP solution                 1e-8 relative
+  golden full SQP                          1e-6 relative, alpha sequence identical
+  notebook closed-loop trace (OSQP, eps 1e-3, vs our exact QP)   2e-6 absolute, first 8 steps
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rbd
+from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("N", [16, 32, 64])
+def test_golden_linearisation_and_qp(lib, model, N):
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+
+    f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
+    s = OSQPSolver(model, N=N)
+    for b in range(f["Pdata"].shape[0]):
+        s.assemble(f["XU_lin"][b], f["xcur"][b], f["goals"][b])
+        for name in ("Pdata", "Adata", "l", "g"):
+            got, ref = getattr(s, name), f[name][b]
+            assert np.abs(got - ref).max() <= 1e-10 * np.abs(ref).max(), name
+    h = lib.Handle(model, N=N, max_batch=f["XU_lin"].shape[0])
+    sol = h.qp(f["XU_lin"], f["xcur"], f["goals"])
+    for b in range(sol.shape[0]):
+        assert _rel(sol[b], f["qp_sol"][b]) < 1e-8
+        np.testing.assert_array_equal(sol[b][:12], f["xcur"][b])  # x_0 = xs exactly
+
+
+@pytest.mark.parametrize("N", [16, 32, 64])
+def test_golden_full_sqp(lib, model, N):
+    f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
+    B = f["XU"].shape[0]
+    h = lib.Handle(model, N=N, max_batch=B)
+    out, st = h.solve(f["xcur"], f["goals"], f["XU"])
+    for b in range(B):
+        assert st["qp_iters"][b] == f["qp_iters"][b]
+        na = st["n_alphas"][b]
+        ref_a = f["alphas"][b][~np.isnan(f["alphas"][b])]
+        np.testing.assert_array_equal(st["alphas"][b][:na], ref_a)
+        ref_s = f["stepsizes"][b][~np.isnan(f["stepsizes"][b])]
+        np.testing.assert_allclose(st["stepsizes"][b][: st["n_steps"][b]], ref_s, rtol=1e-6)
+        assert _rel(out[b], f["sqp_out"][b]) < 1e-6
+
+
+def test_golden_dynamics(lib, model):
+    d = np.load(os.path.join(GOLD, "dynamics.npz"))
+    h = lib.Handle(model, N=16, max_batch=64)
+    dq, dv, Mi, a = h.aba_derivatives(d["q"], d["v"], d["tau"])
+    p, J = h.eepos(d["q"], jacobian=True)
+    for got, ref in ((dq, d["dq"]), (dv, d["dv"]), (Mi, d["Minv"]), (a, d["a"]), (p, d["eepos"]), (J, d["J"])):
+        for i in range(got.shape[0]):
+            assert np.abs(got[i] - ref[i]).max() <= 1e-10 * max(1.0, np.abs(ref[i]).max())
+
+
+def test_notebook_fk_kats(lib, model):
+    kats = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["fk"]
+    h = lib.Handle(model, N=16)
+    p = h.eepos(np.array([k["q"] for k in kats]))
+    for k, pk in zip(kats, p):
+        tol = 0.5 * 10.0 ** (-k["digits"]) * max(1.0, np.abs(k["eepos"]).max()) + 1e-12
+        assert np.abs(pk - np.array(k["eepos"])).max() <= tol
+
+
+def test_mpc_osqp_closed_loop_matches_notebook(lib, model):
+    """The drop-in MPC_OSQP (GPU SQP + GPU rk4 plant) reproduces the reference notebook's
+    printed closed-loop goal distances (notebooks/pin_mpc_indy7.ipynb cell 2)."""
+    from indy7_mpc_amd.osqp_mpc import MPC_OSQP
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    solver = OSQPSolver(model)
+    sqp = SQP_OSQP(solver)
+    ctrl = MPC_OSQP(model, sqp, solver)
+    ends = np.array([solver.eepos(np.array(q)) for q in tr["endpoint_q"]])
+    ctrl.run_mpc(np.array(tr["xstart"]), ends, num_steps=8, verbose=False)
+    d = np.array(ctrl.goal_distances)
+    ref = np.array(tr["goal_distances"][:8])
+    assert abs(d[0] - ref[0]) < 1e-15
+    assert np.abs(d - ref).max() < 2e-6
+    st = sqp.get_stats()
+    assert len(st["qp_iters"]["values"]) == 9  # initial solve + 8 steps
+
+
+def test_sqp_osqp_methods_match_oracle(lib, model):
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+
+    N = 16
+    xcur, goals, XU = synthetic_batch(1, N, seed=12)
+    s = OSQPSolver(model, N=N)
+    sq = SQP_OSQP(s)
+    rs = OSQPSolverRef(N=N)
+    rq = SQPRef(rs)
+    np.testing.assert_allclose(sq.eepos_cost(goals[0], XU[0]), rq.eepos_cost(goals[0], XU[0]), rtol=1e-12)
+    assert abs(sq.integrator_err(XU[0]) - rq.integrator_err(XU[0])) <= 1e-10 * rq.integrator_err(XU[0])
+    sol = s.setup_and_solve_qp(XU[0], xcur[0], goals[0]).x
+    ref = rs.setup_and_solve_qp(XU[0], xcur[0], goals[0]).x
+    assert _rel(sol, ref) < 1e-8
+    assert sq.linesearch(XU[0], sol, goals[0]) == rq.linesearch(XU[0], ref, goals[0])
+    p, J = s.d_eepos(xcur[0][:6])
+    rp, rJ = rbd.d_eepos(xcur[0][:6])
+    np.testing.assert_allclose(J, rJ, atol=1e-13)
+    # compute_dynamics_jacobians fills A_k/B_k/cx_k like the reference
+    q, v, u = XU[0][:6], XU[0][6:12], np.full(6, 3.0)
+    s.compute_dynamics_jacobians(q, v, u)
+    rs.compute_dynamics_jacobians(q, v, u)
+    for n in ("A_k", "B_k", "cx_k"):
+        np.testing.assert_allclose(getattr(s, n), getattr(rs, n), rtol=1e-10, atol=1e-12)
+
+
+def test_batch_invariance_and_independence(lib, model):
+    """Identical problems give identical results (src/gato_mpc_batch.py:124-134), and a
+    problem's result does not depend on its neighbours in the batch."""
+    N, B = 32, 256
+    xcur, goals, XU = synthetic_batch(4, N, seed=31)
+    h = lib.Handle(model, N=N, max_batch=B)
+    idx = np.arange(B) % 4
+    out, st = h.solve(xcur[idx], goals[idx], XU[idx])
+    for b in range(B):
+        np.testing.assert_array_equal(out[b], out[idx[b]])
+    solo, _ = h.solve(xcur[2:3], goals[2:3], XU[2:3])
+    np.testing.assert_array_equal(solo[0], out[2])
+
+
+def test_bench_scale_properties(lib, model):
+    """B=4096, N=32 (the bench config): every solution keeps x_0 = xcur, every stat is in
+    range, and a random sample of problems matches the oracle."""
+    N, B = 32, 4096
+    xcur, goals, XU = synthetic_batch(B, N, seed=45)
+    h = lib.Handle(model, N=N, max_batch=B)
+    out, st = h.solve(xcur, goals, XU)
+    assert np.isfinite(out).all()
+    np.testing.assert_array_equal(out[:, :12], xcur)
+    assert set(np.unique(st["qp_iters"])) <= {1, 2}
+    assert (st["n_alphas"] >= 1).all()
+    allowed = set(SQPRef.ALPHAS.tolist()) | {0.0}
+    for b in range(B):
+        assert set(st["alphas"][b][: st["n_alphas"][b]].tolist()) <= allowed
+    rng = np.random.default_rng(0)
+    for b in rng.choice(B, 6, replace=False):
+        ref = SQPRef(OSQPSolverRef(N=N)).sqp(xcur[b], goals[b], XU[b].copy())
+        assert _rel(out[b], ref) < 1e-6
+
+
+def test_goal_stride_6_equals_stride_3(lib, model):
+    """batch_sqp goal layout (B, 6N), first 3 of each 6 used (gato_controller.py:180-183)."""
+    N, B = 16, 8
+    xcur, goals, XU = synthetic_batch(B, N, seed=8)
+    g6 = np.zeros((B, 6 * N))
+    for k in range(N):
+        g6[:, 6 * k:6 * k + 3] = goals[:, 3 * k:3 * k + 3]
+        g6[:, 6 * k + 3:6 * k + 6] = 123.0  # ignored
+    h = lib.Handle(model, N=N, max_batch=B)
+    o3, _ = h.solve(xcur, goals, XU)
+    o6, _ = h.solve(xcur, g6, XU)
+    np.testing.assert_array_equal(o3, o6)
+
+
+def test_batch_sqp_surface_with_wrench(lib, model):
+    from indy7_mpc_amd.bindings import batch_sqp
+
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, seed=13)
+    g6 = np.zeros((B, 6 * N))
+    for k in range(N):
+        g6[:, 6 * k:6 * k + 3] = goals[:, 3 * k:3 * k + 3]
+    s = batch_sqp.SQPSolverfloat_4()
+    f = np.zeros((B, 6))
+    f[1:, :3] = np.random.default_rng(1).normal(0, 5, (B - 1, 3))
+    s.set_external_wrench_batch(f)
+    s.reset(); s.resetRho(); s.resetLambda()
+    r = s.solve(XU, 0.01, xcur, g6)
+    assert set(r) == {"xu_trajectory", "solve_time_us", "sqp_iterations", "pcg_stats", "line_search_stats"}
+    assert r["xu_trajectory"].shape == (B, 18 * N - 6)
+    # problem 0 has no wrench -> equals the plain solver
+    h = lib.Handle(model, N=N, max_batch=B)
+    plain, _ = h.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(r["xu_trajectory"][0], plain[0])
+    assert not np.array_equal(r["xu_trajectory"][1], plain[1])
+    # sim_forward: one rk4 step per wrench hypothesis, vs the oracle
+    xn = s.sim_forward(xcur[0], np.full(6, 2.0), 0.01)
+    for b in range(B):
+        q, v = rbd.rk4(xcur[0][:6], xcur[0][6:], np.full(6, 2.0), 0.01, fext=[np.zeros(6)] * 5 + [f[b]])
+        np.testing.assert_allclose(xn[b], np.concatenate([q, v]), rtol=1e-10, atol=1e-12)
+
+
+def test_wrench_solve_matches_oracle_dynamics(lib, model):
+    """Linearisation with a local joint-6 wrench == oracle ABA derivatives with f_ext."""
+    N = 16
+    xcur, goals, XU = synthetic_batch(1, N, seed=14)
+    XU = XU + np.random.default_rng(2).normal(0, 0.2, XU.shape)
+    fw = np.array([[3.0, -4.0, 5.0, 0.1, 0.2, -0.3]])
+    h = lib.Handle(model, N=N, max_batch=1)
+    h.set_external_wrench(fw)
+    lin, _ = h.linearize(XU, goals)
+    fext = [np.zeros(6)] * 5 + [fw[0]]
+    for k in (0, 7, N - 2):
+        q, v, u = XU[0][18 * k:18 * k + 6], XU[0][18 * k + 6:18 * k + 12], XU[0][18 * k + 12:18 * k + 18]
+        a = rbd.aba(q, v, u, fext=fext)
+        np.testing.assert_allclose(lin[0, k, 108:], a, rtol=1e-10, atol=1e-9)
+        # complex-step derivative of the wrench-loaded RNEA
+        M = rbd.crba(q)
+        dtq = np.array([np.imag(rbd.rnea(q + 1e-30j * e, v.astype(complex), a.astype(complex), fext=fext)) / 1e-30
+                        for e in np.eye(6)]).T
+        dq = -np.linalg.solve(M, dtq)
+        np.testing.assert_allclose(lin[0, k, :36].reshape(6, 6), 0.01 * dq, rtol=1e-9, atol=1e-11)
+    h.set_external_wrench(None)
+
+
+def test_sharded_solver_matches_single(lib, model):
+    from indy7_mpc_amd.sharding import ShardedSQP
+
+    N, B = 16, 10
+    xcur, goals, XU = synthetic_batch(B, N, seed=15)
+    sh = ShardedSQP(model, devices=[0, 0], N=N, max_batch_per_device=8)
+    out, st = sh.solve(xcur, goals, XU)
+    h = lib.Handle(model, N=N, max_batch=B)
+    ref, rst = h.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(out, ref)
+    np.testing.assert_array_equal(st["qp_iters"], rst["qp_iters"])
+
+
+def test_errors_are_loud(lib, model):
+    h = lib.Handle(model, N=16, max_batch=2)
+    xcur, goals, XU = synthetic_batch(3, 16, seed=1)
+    with pytest.raises(lib.I7MError):
+        h.solve(xcur, goals, XU)  # B > max_batch
+    with pytest.raises(ValueError):
+        h.solve(xcur[:1], goals[:1, :-3], XU[:1])
