@@ -26,35 +26,78 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector = FP64 matrix, AMD spec (not in
 
 
 def algorithmic_bytes(N: int):
-    """Compulsory HBM bytes per problem per launch of each kernel (fp64), and per solve
-    (8*(2*(18N-6) + 12 + 3N) = 312 N)."""
+    """Compulsory HBM bytes per problem per launch of each kernel (fp64): what the kernel must
+    read and write, nothing re-read; and per solve (8*(2*(18N-6)+12+3N) = 312 N)."""
     T = 18 * N - 6
     lin = (N - 1) * 114 * 8
     cost = N * 10 * 8
     return {
         "solve": 8 * (2 * T + 12 + 3 * N),
-        "k_linearize": 8 * (T + 3 * N) + lin + cost,
-        "k_riccati": 8 * (T + 12) + lin + cost + 8 * T,
-        "k_linesearch": 8 * (2 * T + 3 * N) + 8 * T,
+        "k_linearize": 8 * (T + 3 * N) + lin + cost,          # XU, goals -> lin, cost
+        "k_riccati": 8 * (T + 12) + lin + cost + 8 * T,       # XU, xs, lin, cost -> sol
+        "k_linesearch": 8 * (2 * T + 3 * N) + 8 * T,          # XU, sol, goals -> XU
     }
 
 
-def cpu_baseline(N: int, budget_s: float, seed: int):
-    """The numpy oracle (a port of src/osqp_sqp.py + osqp_solver.py with an exact KKT solve)
-    timed single-threaded on a bounded sample of the same workload."""
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
-    from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+def cpu_baseline(N: int, budget_s: float, seed: int, threads: int):
+    """The C++ CPU port (oracle/cpp/i7m_cpu.cpp: the same SQP, exact KKT solve) timed on the
+    host cores on a bounded sample of the same workload, single-threaded and with `threads`
+    OpenMP threads; plus the instrumented flop count of that algorithm on the sample."""
+    from oracle import cpu
+    from oracle.osqp_ref import synthetic_batch
 
-    xcur, goals, XU = synthetic_batch(64, N, seed)
-    solver = OSQPSolverRef(N=N)
-    n = 0
+    n = 64
+    xcur, goals, XU = synthetic_batch(n, N, seed)
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and n < 64:
-        SQPRef(solver).sqp(xcur[n], goals[n], XU[n].copy())
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{n} solves (N={N}, seed {seed}) by oracle/osqp_ref.py (numpy+scipy splu, 1 thread) in {dt:.1f}s"}
+    cpu.solve(xcur[:8], goals[:8], XU[:8], N, nthreads=1)
+    per = (time.perf_counter() - t0) / 8
+    n = int(max(8, min(4096, budget_s / 2 / per)))
+    xcur, goals, XU = synthetic_batch(n, N, seed)
+    t0 = time.perf_counter()
+    cpu.solve(xcur, goals, XU, N, nthreads=1)
+    t1 = time.perf_counter()
+    nm = n * threads
+    xm, gm, Xm = synthetic_batch(nm, N, seed)
+    t2 = time.perf_counter()
+    cpu.solve(xm, gm, Xm, N, nthreads=threads)
+    t3 = time.perf_counter()
+    fl = [cpu.count_flops(xcur[b], goals[b], XU[b], N) for b in range(min(n, 64))]
+    per_iter_lin = fl[0]["linearize"] / fl[0]["iters"]
+    per_iter_qp = fl[0]["qp"] / fl[0]["iters"]
+    return {
+        "value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
+        "sample": f"{n} solves (config-3 draws, N={N}, seed {seed}) by oracle/cpp/i7m_cpu.cpp, 1 thread, "
+                  f"{t1 - t0:.1f}s",
+        "all_cores": {"value": nm / (t3 - t2), "cores": threads, "sample": f"{nm} solves, {threads} OpenMP threads"},
+        "cpu_model": _cpu_model(),
+        "flops": {"per_solve_mean": float(np.mean([f["total"] for f in fl])),
+                  "linearize_per_iter": per_iter_lin, "riccati_per_iter": per_iter_qp,
+                  "linesearch_per_solve_mean": float(np.mean([f["linesearch"] for f in fl])),
+                  "merit_evals_mean": float(np.mean([f["merit_evals"] for f in fl]))},
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _pmc_traffic(kernel: str, B: int, N: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json,
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, x1024) for this kernel/config, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(f"{kernel}:B{B}:N{N}")
+        return None if e is None else e["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -64,7 +107,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
     ap.add_argument("--N", type=int, default=32)
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=30)
     args = ap.parse_args()
@@ -156,9 +200,14 @@ def main():
     dom = max(ktimes, key=lambda k: ktimes[k][0])
     dom_ms, dom_cnt = ktimes[dom]
     dom_avg_s = dom_ms / max(dom_cnt, 1) / 1e3
-    achieved = B * ab[dom] / dom_avg_s / 1e9
-    per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c, "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)}
-                  for k, (ms, c) in ktimes.items()}
+    # problems a launch actually processes: iteration 2 only runs the problems still active
+    launches_per_step = max(dom_cnt // args.steps, 1)
+    problems_per_launch = float(st["qp_iters"].sum()) / launches_per_step
+    achieved = problems_per_launch * ab[dom] / dom_avg_s / 1e9
+    traffic = _pmc_traffic(dom, B, N)
+    per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c,
+                      "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)} for k, (ms, c) in ktimes.items()}
+    cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads)
     out = {
         "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
         "value": value,
@@ -179,14 +228,27 @@ def main():
         "qp_iters_mean": qp_iters_mean,
         "kernels": per_kernel,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "algorithmic_bytes_per_problem": ab[dom]},
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "algorithmic_bytes_per_problem": ab[dom], "problems_per_launch": problems_per_launch,
+                     "avg_launch_us": dom_avg_s * 1e6},
         "roofline_solve": {"bound": "hbm", "achieved": value * ab["solve"] / 1e9, "peak": HBM_PEAK_GBS * world,
                            "unit": "GB/s", "frac": value * ab["solve"] / 1e9 / (HBM_PEAK_GBS * world),
                            "bytes_per_solve": ab["solve"]},
     }
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(N, args.cpu_budget, seed)
+    if cpu is not None:
+        fl = cpu.pop("flops")
+        fl_dom = {"k_linearize": fl["linearize_per_iter"], "k_riccati": fl["riccati_per_iter"]}.get(dom)
+        if fl_dom is not None:
+            a_tf = problems_per_launch * fl_dom / dom_avg_s / 1e12
+            out["roofline_fp64"] = {"bound": "fp64", "kernel": dom, "achieved": a_tf, "peak": FP64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": a_tf / FP64_PEAK_TFLOPS,
+                                    "flops_per_problem": fl_dom}
+        out["solve_fp64"] = {"achieved": value * fl["per_solve_mean"] / 1e12, "unit": "TFLOP/s",
+                             "peak": FP64_PEAK_TFLOPS * world,
+                             "frac": value * fl["per_solve_mean"] / 1e12 / (FP64_PEAK_TFLOPS * world),
+                             "flops_per_solve": fl["per_solve_mean"], "merit_evals_per_solve": fl["merit_evals_mean"]}
+        out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -1,0 +1,657 @@
+// ORACLE (test/bench infrastructure only) — C++ CPU restatement of the reference hot path.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this; the
+// product (indy7_mpc_amd) never does.  Two uses:
+//   * bench.py's CPU baseline ("port"): the same SQP as src/osqp_sqp.py:76-93 with the QP of
+//     src/osqp_solver.py:137-143 solved exactly, timed on the host cores (OpenMP over problems);
+//   * the instrumented flop count of that algorithm (template on an op-counting scalar) that
+//     bench.py's FP64 roofline uses (SURVEY.md §8d asks for an instrumented count).
+// Follows, function by function:
+//   rnea / crba / forward_dynamics   pin.aba / computeABADerivatives (src/osqp_solver.py:71-77,
+//                                    src/osqp_sqp.py:40) — local-frame RNEA, forward-mode dual
+//                                    tangents for the derivatives (da/dx = -Minv dRNEA/dx)
+//   fk_jac                           eepos / d_eepos (src/osqp_solver.py:146-155)
+//   linearize                        update_constraint_matrix / update_cost_matrix (:83-135)
+//   riccati                          the equality-constrained QP (:137-143), exact
+//   merit / linesearch               eepos_cost, integrator_err, linesearch (src/osqp_sqp.py:13-74)
+//   sqp                              src/osqp_sqp.py:76-93
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- op-counting scalar
+struct CountD {
+  double v;
+  static thread_local uint64_t flops;
+  CountD() : v(0) {}
+  CountD(double x) : v(x) {}
+};
+thread_local uint64_t CountD::flops = 0;
+inline CountD operator+(CountD a, CountD b) { ++CountD::flops; return CountD(a.v + b.v); }
+inline CountD operator-(CountD a, CountD b) { ++CountD::flops; return CountD(a.v - b.v); }
+inline CountD operator*(CountD a, CountD b) { ++CountD::flops; return CountD(a.v * b.v); }
+inline CountD operator/(CountD a, CountD b) { ++CountD::flops; return CountD(a.v / b.v); }
+inline CountD operator-(CountD a) { return CountD(-a.v); }
+inline CountD& operator+=(CountD& a, CountD b) { a = a + b; return a; }
+inline CountD& operator-=(CountD& a, CountD b) { a = a - b; return a; }
+inline bool operator<(CountD a, CountD b) { return a.v < b.v; }
+inline bool operator<=(CountD a, CountD b) { return a.v <= b.v; }
+inline CountD sqrt(CountD a) { ++CountD::flops; return CountD(std::sqrt(a.v)); }
+inline CountD fabs(CountD a) { return CountD(std::fabs(a.v)); }
+inline void sincos2(CountD q, CountD* s, CountD* c) { CountD::flops += 2; *s = std::sin(q.v); *c = std::cos(q.v); }
+inline void sincos2(double q, double* s, double* c) { *s = std::sin(q); *c = std::cos(q); }
+inline double val(double x) { return x; }
+inline double val(CountD x) { return x.v; }
+using std::sqrt;
+using std::fabs;
+
+template <class R>
+struct Dual {
+  R v, d;
+  Dual() : v(0), d(0) {}
+  Dual(R a) : v(a), d(0) {}
+  Dual(R a, R b) : v(a), d(b) {}
+};
+template <class R> inline Dual<R> operator+(Dual<R> a, Dual<R> b) { return {a.v + b.v, a.d + b.d}; }
+template <class R> inline Dual<R> operator-(Dual<R> a, Dual<R> b) { return {a.v - b.v, a.d - b.d}; }
+template <class R> inline Dual<R> operator*(Dual<R> a, Dual<R> b) { return {a.v * b.v, a.v * b.d + a.d * b.v}; }
+template <class R> inline Dual<R> operator*(R a, Dual<R> b) { return {a * b.v, a * b.d}; }
+
+struct Model {
+  double Rp[6][9], tp[6][3], m[6], h[6][3], Io[6][6], g[3];
+};
+
+Model make_model(const double* p) {
+  // packed layout == i7m_model (include/indy7_mpc.h)
+  Model M;
+  const double* R = p;
+  const double* t = p + 54;
+  const double* mass = p + 72;
+  const double* com = p + 78;
+  const double* I = p + 96;
+  const double* g = p + 132;
+  for (int i = 0; i < 6; ++i) {
+    for (int k = 0; k < 9; ++k) M.Rp[i][k] = R[9 * i + k];
+    for (int k = 0; k < 3; ++k) M.tp[i][k] = t[3 * i + k];
+    M.m[i] = mass[i];
+    const double* c = com + 3 * i;
+    for (int k = 0; k < 3; ++k) M.h[i][k] = mass[i] * c[k];
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    const double* Ic = I + 6 * i;
+    M.Io[i][0] = Ic[0] + mass[i] * (cc - c[0] * c[0]);
+    M.Io[i][1] = Ic[1] - mass[i] * c[0] * c[1];
+    M.Io[i][2] = Ic[2] - mass[i] * c[0] * c[2];
+    M.Io[i][3] = Ic[3] + mass[i] * (cc - c[1] * c[1]);
+    M.Io[i][4] = Ic[4] - mass[i] * c[1] * c[2];
+    M.Io[i][5] = Ic[5] + mass[i] * (cc - c[2] * c[2]);
+  }
+  for (int k = 0; k < 3; ++k) M.g[k] = g[k];
+  return M;
+}
+
+// Local-frame RNEA on scalar type T (R or Dual<R>) with base scalar R for constants.
+template <class R, class T>
+void rnea(const Model& M, const T* c, const T* s, const T* qd, const T* qdd, bool grav, const double* f6, T* tau) {
+  auto K = [](double x) -> T { return T(R(x)); };
+  T vl[3] = {K(0), K(0), K(0)}, vw[3] = {K(0), K(0), K(0)};
+  T al[3] = {K(grav ? -M.g[0] : 0), K(grav ? -M.g[1] : 0), K(grav ? -M.g[2] : 0)}, aw[3] = {K(0), K(0), K(0)};
+  T f[6][6];
+  for (int i = 0; i < 6; ++i) {
+    const double* Rp = M.Rp[i];
+    const double* t = M.tp[i];
+    auto to_child = [&](T* l, T* w) {
+      T x0 = l[0] - (K(t[1]) * w[2] - K(t[2]) * w[1]);
+      T x1 = l[1] - (K(t[2]) * w[0] - K(t[0]) * w[2]);
+      T x2 = l[2] - (K(t[0]) * w[1] - K(t[1]) * w[0]);
+      T y0 = K(Rp[0]) * x0 + K(Rp[3]) * x1 + K(Rp[6]) * x2;
+      T y1 = K(Rp[1]) * x0 + K(Rp[4]) * x1 + K(Rp[7]) * x2;
+      T y2 = K(Rp[2]) * x0 + K(Rp[5]) * x1 + K(Rp[8]) * x2;
+      T z0 = K(Rp[0]) * w[0] + K(Rp[3]) * w[1] + K(Rp[6]) * w[2];
+      T z1 = K(Rp[1]) * w[0] + K(Rp[4]) * w[1] + K(Rp[7]) * w[2];
+      T z2 = K(Rp[2]) * w[0] + K(Rp[5]) * w[1] + K(Rp[8]) * w[2];
+      l[0] = c[i] * y0 + s[i] * y1; l[1] = c[i] * y1 - s[i] * y0; l[2] = y2;
+      w[0] = c[i] * z0 + s[i] * z1; w[1] = c[i] * z1 - s[i] * z0; w[2] = z2;
+    };
+    to_child(vl, vw);
+    to_child(al, aw);
+    vw[2] = vw[2] + qd[i];
+    al[0] = al[0] + vl[1] * qd[i];
+    al[1] = al[1] - vl[0] * qd[i];
+    aw[0] = aw[0] + vw[1] * qd[i];
+    aw[1] = aw[1] - vw[0] * qd[i];
+    aw[2] = aw[2] + qdd[i];
+    auto imul = [&](const T* l, const T* w, T* fl, T* fn) {
+      const double m = M.m[i];
+      const double* h = M.h[i];
+      const double* I = M.Io[i];
+      fl[0] = K(m) * l[0] - (K(h[1]) * w[2] - K(h[2]) * w[1]);
+      fl[1] = K(m) * l[1] - (K(h[2]) * w[0] - K(h[0]) * w[2]);
+      fl[2] = K(m) * l[2] - (K(h[0]) * w[1] - K(h[1]) * w[0]);
+      fn[0] = K(I[0]) * w[0] + K(I[1]) * w[1] + K(I[2]) * w[2] + (K(h[1]) * l[2] - K(h[2]) * l[1]);
+      fn[1] = K(I[1]) * w[0] + K(I[3]) * w[1] + K(I[4]) * w[2] + (K(h[2]) * l[0] - K(h[0]) * l[2]);
+      fn[2] = K(I[2]) * w[0] + K(I[4]) * w[1] + K(I[5]) * w[2] + (K(h[0]) * l[1] - K(h[1]) * l[0]);
+    };
+    T hl[3], hn[3], il[3], in[3];
+    imul(vl, vw, hl, hn);
+    imul(al, aw, il, in);
+    f[i][0] = il[0] + (vw[1] * hl[2] - vw[2] * hl[1]);
+    f[i][1] = il[1] + (vw[2] * hl[0] - vw[0] * hl[2]);
+    f[i][2] = il[2] + (vw[0] * hl[1] - vw[1] * hl[0]);
+    f[i][3] = in[0] + (vw[1] * hn[2] - vw[2] * hn[1]) + (vl[1] * hl[2] - vl[2] * hl[1]);
+    f[i][4] = in[1] + (vw[2] * hn[0] - vw[0] * hn[2]) + (vl[2] * hl[0] - vl[0] * hl[2]);
+    f[i][5] = in[2] + (vw[0] * hn[1] - vw[1] * hn[0]) + (vl[0] * hl[1] - vl[1] * hl[0]);
+  }
+  if (f6)
+    for (int k = 0; k < 6; ++k) f[5][k] = f[5][k] - K(f6[k]);
+  for (int i = 5; i >= 0; --i) {
+    tau[i] = f[i][5];
+    if (i == 0) break;
+    const double* Rp = M.Rp[i];
+    const double* t = M.tp[i];
+    T x0 = c[i] * f[i][0] - s[i] * f[i][1], x1 = s[i] * f[i][0] + c[i] * f[i][1], x2 = f[i][2];
+    T F0 = K(Rp[0]) * x0 + K(Rp[1]) * x1 + K(Rp[2]) * x2;
+    T F1 = K(Rp[3]) * x0 + K(Rp[4]) * x1 + K(Rp[5]) * x2;
+    T F2 = K(Rp[6]) * x0 + K(Rp[7]) * x1 + K(Rp[8]) * x2;
+    x0 = c[i] * f[i][3] - s[i] * f[i][4]; x1 = s[i] * f[i][3] + c[i] * f[i][4]; x2 = f[i][5];
+    T N0 = K(Rp[0]) * x0 + K(Rp[1]) * x1 + K(Rp[2]) * x2;
+    T N1 = K(Rp[3]) * x0 + K(Rp[4]) * x1 + K(Rp[5]) * x2;
+    T N2 = K(Rp[6]) * x0 + K(Rp[7]) * x1 + K(Rp[8]) * x2;
+    f[i - 1][0] = f[i - 1][0] + F0;
+    f[i - 1][1] = f[i - 1][1] + F1;
+    f[i - 1][2] = f[i - 1][2] + F2;
+    f[i - 1][3] = f[i - 1][3] + N0 + (K(t[1]) * F2 - K(t[2]) * F1);
+    f[i - 1][4] = f[i - 1][4] + N1 + (K(t[2]) * F0 - K(t[0]) * F2);
+    f[i - 1][5] = f[i - 1][5] + N2 + (K(t[0]) * F1 - K(t[1]) * F0);
+  }
+}
+
+template <class R>
+void chol6(R A[6][6]) {
+  for (int j = 0; j < 6; ++j) {
+    R d = A[j][j];
+    for (int k = 0; k < j; ++k) d = d - A[j][k] * A[j][k];
+    d = sqrt(d);
+    A[j][j] = d;
+    for (int i = j + 1; i < 6; ++i) {
+      R v = A[i][j];
+      for (int k = 0; k < j; ++k) v = v - A[i][k] * A[j][k];
+      A[i][j] = v / d;
+    }
+  }
+}
+template <class R>
+void chol6_solve(const R L[6][6], R* b) {
+  for (int i = 0; i < 6; ++i) {
+    R v = b[i];
+    for (int k = 0; k < i; ++k) v = v - L[i][k] * b[k];
+    b[i] = v / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    R v = b[i];
+    for (int k = i + 1; k < 6; ++k) v = v - L[k][i] * b[k];
+    b[i] = v / L[i][i];
+  }
+}
+
+// Composite-rigid-body M(q) (same recursion as the GPU's crba), then a = M^-1 (tau - b).
+template <class R>
+void crba(const Model& Md, const R* c, const R* s, R Mq[6][6]) {
+  R cm[6], ch[6][3], cI[6][6];
+  for (int i = 0; i < 6; ++i) {
+    cm[i] = R(Md.m[i]);
+    for (int k = 0; k < 3; ++k) ch[i][k] = R(Md.h[i][k]);
+    for (int k = 0; k < 6; ++k) cI[i][k] = R(Md.Io[i][k]);
+  }
+  for (int i = 5; i >= 0; --i) {
+    R fl[3] = {R(0) - ch[i][1], ch[i][0], R(0)};
+    R fn[3] = {cI[i][2], cI[i][4], cI[i][5]};
+    Mq[i][i] = fn[2];
+    for (int j = i; j >= 1; --j) {
+      const double* Rp = Md.Rp[j];
+      const double* t = Md.tp[j];
+      R x0 = c[j] * fl[0] - s[j] * fl[1], x1 = s[j] * fl[0] + c[j] * fl[1], x2 = fl[2];
+      R F0 = R(Rp[0]) * x0 + R(Rp[1]) * x1 + R(Rp[2]) * x2;
+      R F1 = R(Rp[3]) * x0 + R(Rp[4]) * x1 + R(Rp[5]) * x2;
+      R F2 = R(Rp[6]) * x0 + R(Rp[7]) * x1 + R(Rp[8]) * x2;
+      x0 = c[j] * fn[0] - s[j] * fn[1]; x1 = s[j] * fn[0] + c[j] * fn[1]; x2 = fn[2];
+      R N0 = R(Rp[0]) * x0 + R(Rp[1]) * x1 + R(Rp[2]) * x2;
+      R N1 = R(Rp[3]) * x0 + R(Rp[4]) * x1 + R(Rp[5]) * x2;
+      R N2 = R(Rp[6]) * x0 + R(Rp[7]) * x1 + R(Rp[8]) * x2;
+      fn[0] = N0 + (R(t[1]) * F2 - R(t[2]) * F1);
+      fn[1] = N1 + (R(t[2]) * F0 - R(t[0]) * F2);
+      fn[2] = N2 + (R(t[0]) * F1 - R(t[1]) * F0);
+      fl[0] = F0; fl[1] = F1; fl[2] = F2;
+      Mq[i][j - 1] = fn[2];
+      Mq[j - 1][i] = fn[2];
+    }
+    if (i > 0) {
+      const double* Rp = Md.Rp[i];
+      const double* t = Md.tp[i];
+      const R m = cm[i];
+      R hz[3] = {c[i] * ch[i][0] - s[i] * ch[i][1], s[i] * ch[i][0] + c[i] * ch[i][1], ch[i][2]};
+      R hr[3];
+      for (int r = 0; r < 3; ++r) hr[r] = R(Rp[3 * r]) * hz[0] + R(Rp[3 * r + 1]) * hz[1] + R(Rp[3 * r + 2]) * hz[2];
+      const R* I = cI[i];
+      const R cc = c[i] * c[i], ss = s[i] * s[i], cs = c[i] * s[i];
+      R A[3][3];
+      A[0][0] = cc * I[0] - R(2.0) * cs * I[1] + ss * I[3];
+      A[1][1] = ss * I[0] + R(2.0) * cs * I[1] + cc * I[3];
+      A[0][1] = cs * (I[0] - I[3]) + (cc - ss) * I[1];
+      A[0][2] = c[i] * I[2] - s[i] * I[4];
+      A[1][2] = s[i] * I[2] + c[i] * I[4];
+      A[2][2] = I[5];
+      A[1][0] = A[0][1]; A[2][0] = A[0][2]; A[2][1] = A[1][2];
+      R RA[3][3], Bm[3][3];
+      for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) RA[r][q] = R(Rp[3 * r]) * A[0][q] + R(Rp[3 * r + 1]) * A[1][q] + R(Rp[3 * r + 2]) * A[2][q];
+      for (int r = 0; r < 3; ++r)
+        for (int q = r; q < 3; ++q) Bm[r][q] = RA[r][0] * R(Rp[3 * q]) + RA[r][1] * R(Rp[3 * q + 1]) + RA[r][2] * R(Rp[3 * q + 2]);
+      const R ht = hr[0] * R(t[0]) + hr[1] * R(t[1]) + hr[2] * R(t[2]);
+      const R tt = R(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+      const R dg = R(2.0) * ht + m * tt;
+      const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+      for (int k = 0; k < 6; ++k) {
+        const int r = iu[k][0], q = iu[k][1];
+        R v = Bm[r][q] - (R(t[r]) * hr[q] + hr[r] * R(t[q])) - m * R(t[r]) * R(t[q]);
+        if (r == q) v = v + dg;
+        cI[i - 1][k] = cI[i - 1][k] + v;
+      }
+      for (int k = 0; k < 3; ++k) ch[i - 1][k] = ch[i - 1][k] + hr[k] + m * R(t[k]);
+      cm[i - 1] = cm[i - 1] + m;
+    }
+  }
+}
+
+template <class R>
+void forward_dynamics(const Model& Md, const R* c, const R* s, const R* v, const R* tau, const double* f6, R L[6][6],
+                      R* a) {
+  R z[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+  crba(Md, c, s, L);
+  chol6(L);
+  R b[6];
+  rnea<R, R>(Md, c, s, v, z, true, f6, b);
+  for (int i = 0; i < 6; ++i) a[i] = tau[i] - b[i];
+  chol6_solve(L, a);
+}
+
+template <class R>
+void fk_jac(const Model& Md, const R* c, const R* s, R* p, R J[3][6]) {
+  R Rw[3][3] = {{R(1), R(0), R(0)}, {R(0), R(1), R(0)}, {R(0), R(0), R(1)}};
+  R pos[3] = {R(0), R(0), R(0)}, zs[6][3], ps[6][3];
+  for (int i = 0; i < 6; ++i) {
+    const double* Rp = Md.Rp[i];
+    const double* t = Md.tp[i];
+    R np_[3], RR[3][3];
+    for (int r = 0; r < 3; ++r) np_[r] = pos[r] + Rw[r][0] * R(t[0]) + Rw[r][1] * R(t[1]) + Rw[r][2] * R(t[2]);
+    for (int r = 0; r < 3; ++r)
+      for (int q = 0; q < 3; ++q) RR[r][q] = Rw[r][0] * R(Rp[q]) + Rw[r][1] * R(Rp[3 + q]) + Rw[r][2] * R(Rp[6 + q]);
+    for (int r = 0; r < 3; ++r) {
+      Rw[r][0] = RR[r][0] * c[i] + RR[r][1] * s[i];
+      Rw[r][1] = RR[r][1] * c[i] - RR[r][0] * s[i];
+      Rw[r][2] = RR[r][2];
+      zs[i][r] = RR[r][2];
+      ps[i][r] = np_[r];
+      pos[r] = np_[r];
+    }
+  }
+  for (int r = 0; r < 3; ++r) p[r] = pos[r];
+  if (J)
+    for (int j = 0; j < 6; ++j) {
+      R d0 = pos[0] - ps[j][0], d1 = pos[1] - ps[j][1], d2 = pos[2] - ps[j][2];
+      J[0][j] = zs[j][1] * d2 - zs[j][2] * d1;
+      J[1][j] = zs[j][2] * d0 - zs[j][0] * d2;
+      J[2][j] = zs[j][0] * d1 - zs[j][1] * d0;
+    }
+}
+
+struct Params {
+  int N, regularize, max_iters, goal_stride;
+  double dt, dQ, R, QN, eps, mu, step_tol;
+};
+
+template <class R>
+struct Solver {
+  const Model& Md;
+  Params P;
+  int T;
+  std::vector<R> lin, cost, K, sol;  // lin (N-1)*114, cost N*10, K (N-1)*84
+  Solver(const Model& m, const Params& p) : Md(m), P(p), T(18 * p.N - 6) {
+    lin.resize((P.N - 1) * 114);
+    cost.resize(P.N * 10);
+    K.resize((P.N - 1) * 84);
+    sol.resize(T);
+  }
+
+  void linearize(const R* X, const double* goal, const double* f6) {
+    const R dt = R(P.dt);
+    for (int k = 0; k < P.N - 1; ++k) {
+      const R* x = X + 18 * k;
+      R c[6], s[6], L[6][6], a[6];
+      for (int i = 0; i < 6; ++i) sincos2(x[i], &s[i], &c[i]);
+      forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
+      R* o = &lin[114 * k];
+      for (int d = 0; d < 12; ++d) {
+        Dual<R> dc[6], ds[6], dv[6], da[6], dtau[6];
+        for (int i = 0; i < 6; ++i) {
+          dc[i] = {c[i], d == i ? R(0) - s[i] : R(0)};
+          ds[i] = {s[i], d == i ? c[i] : R(0)};
+          dv[i] = {x[6 + i], (d - 6 == i) ? R(1) : R(0)};
+          da[i] = {a[i], R(0)};
+        }
+        rnea<R, Dual<R>>(Md, dc, ds, dv, da, true, f6, dtau);
+        R col[6];
+        for (int i = 0; i < 6; ++i) col[i] = R(0) - dtau[i].d;
+        chol6_solve(L, col);
+        for (int i = 0; i < 6; ++i) {
+          if (d < 6) o[6 * i + d] = dt * col[i];
+          else o[36 + 6 * i + d - 6] = (i == d - 6 ? R(1) : R(0)) + dt * col[i];
+        }
+      }
+      for (int d = 0; d < 6; ++d) {
+        R e[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+        e[d] = R(1);
+        chol6_solve(L, e);
+        for (int i = 0; i <= d; ++i) o[72 + 6 * i + d] = o[72 + 6 * d + i] = dt * e[i];
+      }
+      for (int i = 0; i < 6; ++i) o[108 + i] = a[i];
+    }
+    for (int k = 0; k < P.N; ++k) {
+      const R* q = X + 18 * k;
+      R c[6], s[6], p[3], J[3][6];
+      for (int i = 0; i < 6; ++i) sincos2(q[i], &s[i], &c[i]);
+      fk_jac(Md, c, s, p, J);
+      const double* g = goal + (size_t)k * P.goal_stride;
+      R e0 = p[0] - R(g[0]), e1 = p[1] - R(g[1]), e2 = p[2] - R(g[2]);
+      R nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      R w = P.regularize ? R(1) / (fabs(nrm) + R(P.eps)) : R(1);
+      R* o = &cost[10 * k];
+      for (int j = 0; j < 6; ++j) o[j] = e0 * J[0][j] + e1 * J[1][j] + e2 * J[2][j];
+      o[6] = R(k == P.N - 1 ? P.QN : 1.0);
+      o[7] = R(P.dQ) * w;
+      o[8] = R(P.R) * w;
+      o[9] = nrm;
+    }
+  }
+
+  void riccati(const R* X, const R* xs) {
+    const int N = P.N;
+    const R dt = R(P.dt);
+    R V[12][12], v[12];
+    const R* cw = &cost[10 * (N - 1)];
+    for (int r = 0; r < 12; ++r)
+      for (int c = 0; c < 12; ++c) V[r][c] = (r < 6 && c < 6) ? cw[6] * (cw[r] * cw[c]) : (r == c ? cw[7] : R(0));
+    for (int r = 0; r < 12; ++r) v[r] = r < 6 ? cw[6] * cw[r] : cw[7] * X[18 * (N - 1) + r];
+    for (int k = N - 2; k >= 0; --k) {
+      const R* L = &lin[114 * k];
+      const R* w = &cost[10 * k];
+      const R* x = X + 18 * k;
+      const R *Aq = L, *Av = L + 36, *Bu = L + 72, *a = L + 108;
+      R cv[6];
+      for (int i = 0; i < 6; ++i) {
+        R acc = R(0);
+        for (int j = 0; j < 6; ++j) acc = acc + Aq[6 * i + j] * x[j] + Av[6 * i + j] * x[6 + j] + Bu[6 * i + j] * x[12 + j];
+        cv[i] = (x[6 + i] + a[i] * dt) - acc;
+      }
+      R VA[12][12], Tm[6][6], s_[12];
+      for (int r = 0; r < 12; ++r) {
+        for (int c = 0; c < 6; ++c) {
+          R a1 = V[r][c], a2 = dt * V[r][c];
+          for (int m = 0; m < 6; ++m) {
+            a1 = a1 + V[r][6 + m] * Aq[6 * m + c];
+            a2 = a2 + V[r][6 + m] * Av[6 * m + c];
+          }
+          VA[r][c] = a1;
+          VA[r][6 + c] = a2;
+        }
+        R acc = v[r];
+        for (int m = 0; m < 6; ++m) acc = acc + V[r][6 + m] * cv[m];
+        s_[r] = acc;
+      }
+      for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c) {
+          R acc = R(0);
+          for (int m = 0; m < 6; ++m) acc = acc + V[6 + r][6 + m] * Bu[6 * m + c];
+          Tm[r][c] = acc;
+        }
+      R AtVA[12][12], G[6][12], H[6][6], h[6], vA[12];
+      for (int r = 0; r < 12; ++r)
+        for (int c = r; c < 12; ++c) {
+          R acc = r < 6 ? VA[r][c] : dt * VA[r - 6][c];
+          for (int m = 0; m < 6; ++m) acc = acc + (r < 6 ? Aq[6 * m + r] : Av[6 * m + r - 6]) * VA[6 + m][c];
+          AtVA[r][c] = AtVA[c][r] = acc;
+        }
+      for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 12; ++c) {
+          R acc = R(0);
+          for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * VA[6 + m][c];
+          G[r][c] = acc;
+        }
+      for (int r = 0; r < 6; ++r)
+        for (int c = r; c < 6; ++c) {
+          R acc = r == c ? w[8] : R(0);
+          for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * Tm[m][c];
+          H[r][c] = H[c][r] = acc;
+        }
+      for (int r = 0; r < 6; ++r) {
+        R acc = w[8] * x[12 + r];
+        for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * s_[6 + m];
+        h[r] = acc;
+      }
+      for (int r = 0; r < 12; ++r) {
+        R acc = r < 6 ? w[6] * w[r] + s_[r] : w[7] * x[6 + r - 6] + dt * s_[r - 6];
+        for (int m = 0; m < 6; ++m) acc = acc + (r < 6 ? Aq[6 * m + r] : Av[6 * m + r - 6]) * s_[6 + m];
+        vA[r] = acc;
+      }
+      chol6(H);
+      R* Kk = &K[84 * k];
+      for (int c = 0; c < 13; ++c) {
+        R rhs[6];
+        for (int i = 0; i < 6; ++i) rhs[i] = c < 12 ? G[i][c] : h[i];
+        chol6_solve(H, rhs);
+        for (int i = 0; i < 6; ++i) Kk[c < 12 ? 12 * i + c : 72 + i] = R(0) - rhs[i];
+      }
+      for (int i = 0; i < 6; ++i) Kk[78 + i] = cv[i];
+      for (int r = 0; r < 12; ++r)
+        for (int c = r; c < 12; ++c) {
+          R acc = AtVA[r][c];
+          if (r < 6 && c < 6) acc = acc + w[6] * (w[r] * w[c]);
+          else if (r == c) acc = acc + w[7];
+          for (int m = 0; m < 6; ++m) acc = acc + G[m][r] * Kk[12 * m + c];
+          V[r][c] = V[c][r] = acc;
+        }
+      for (int r = 0; r < 12; ++r) {
+        R acc = vA[r];
+        for (int m = 0; m < 6; ++m) acc = acc + G[m][r] * Kk[72 + m];
+        v[r] = acc;
+      }
+    }
+    R xk[12];
+    for (int i = 0; i < 12; ++i) sol[i] = xk[i] = xs[i];
+    for (int k = 0; k < N - 1; ++k) {
+      const R* Kk = &K[84 * k];
+      const R* L = &lin[114 * k];
+      R u[6];
+      for (int i = 0; i < 6; ++i) {
+        R acc = Kk[72 + i];
+        for (int j = 0; j < 12; ++j) acc = acc + Kk[12 * i + j] * xk[j];
+        u[i] = acc;
+        sol[18 * k + 12 + i] = acc;
+      }
+      R xn[12];
+      for (int i = 0; i < 6; ++i) {
+        xn[i] = xk[i] + dt * xk[6 + i];
+        R acc = Kk[78 + i];
+        for (int j = 0; j < 6; ++j) acc = acc + L[6 * i + j] * xk[j] + L[36 + 6 * i + j] * xk[6 + j] + L[72 + 6 * i + j] * u[j];
+        xn[6 + i] = acc;
+      }
+      for (int i = 0; i < 12; ++i) sol[18 * (k + 1) + i] = xk[i] = xn[i];
+    }
+  }
+
+  // merit of Xn (initial-state term relative to X0)
+  R merit(const R* Xn, const R* X0, const double* goal, const double* f6) {
+    R qc = R(0), vc = R(0), uc = R(0), cv = R(0);
+    const R dt = R(P.dt);
+    for (int k = 0; k < P.N; ++k) {
+      const R* x = Xn + 18 * k;
+      R c[6], s[6], p[3];
+      for (int i = 0; i < 6; ++i) sincos2(x[i], &s[i], &c[i]);
+      fk_jac(Md, c, s, p, (R(*)[6]) nullptr);
+      const double* g = goal + (size_t)k * P.goal_stride;
+      R e0 = p[0] - R(g[0]), e1 = p[1] - R(g[1]), e2 = p[2] - R(g[2]);
+      qc = qc + R(k == P.N - 1 ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
+      R vv = R(0);
+      for (int i = 0; i < 6; ++i) vv = vv + x[6 + i] * x[6 + i];
+      vc = vc + R(P.dQ) * vv;
+      if (k < P.N - 1) {
+        R uu = R(0);
+        for (int i = 0; i < 6; ++i) uu = uu + x[12 + i] * x[12 + i];
+        uc = uc + R(P.R) * uu;
+        R L[6][6], a[6];
+        forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
+        const R* xn = Xn + 18 * (k + 1);
+        R eq = R(0), ev = R(0);
+        for (int i = 0; i < 6; ++i) {
+          R dq = (x[i] + x[6 + i] * dt) - xn[i];
+          R dv = (x[6 + i] + a[i] * dt) - xn[6 + i];
+          eq = eq + dq * dq;
+          ev = ev + dv * dv;
+        }
+        cv = cv + (sqrt(eq) + sqrt(ev));
+      }
+    }
+    R d0 = R(0);
+    for (int i = 0; i < 12; ++i) d0 = d0 + (Xn[i] - X0[i]) * (Xn[i] - X0[i]);
+    cv = cv + sqrt(d0);
+    return qc + vc + uc + R(P.mu) * cv;
+  }
+
+  // returns qp_iters; alphas/steps filled
+  int sqp(R* X, const R* xs, const double* goal, const double* f6, double* alphas, double* steps, int* n_alpha,
+          int* n_step) {
+    static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
+    std::vector<R> Xn(T);
+    *n_alpha = *n_step = 0;
+    int qp = 0;
+    for (qp = 0; qp < P.max_iters; ++qp) {
+      linearize(X, goal, f6);
+      riccati(X, xs);
+      R base = merit(X, X, goal, f6);
+      double alpha = 0.0;
+      for (int ai = 0; ai < 8; ++ai) {
+        for (int e = 0; e < T; ++e) Xn[e] = X[e] + R(AL[ai]) * (sol[e] - X[e]);
+        if (merit(Xn.data(), X, goal, f6) <= base) {
+          alpha = AL[ai];
+          break;
+        }
+      }
+      alphas[(*n_alpha)++] = alpha;
+      if (alpha == 0.0) continue;
+      R ss = R(0);
+      for (int e = 0; e < T; ++e) {
+        R stp = R(alpha) * (sol[e] - X[e]);
+        X[e] = X[e] + stp;
+        ss = ss + stp * stp;
+      }
+      const double stepsize = val(sqrt(ss));
+      steps[(*n_step)++] = stepsize;
+      if (stepsize < P.step_tol) break;
+    }
+    return qp < P.max_iters ? qp + 1 : P.max_iters;
+  }
+};
+
+Params make_params(int N, const double* cfg, int goal_stride) {
+  // cfg: dt, dQ, R, QN, eps, mu, step_tol, regularize, max_iters
+  Params P;
+  P.N = N;
+  P.dt = cfg[0]; P.dQ = cfg[1]; P.R = cfg[2]; P.QN = cfg[3]; P.eps = cfg[4]; P.mu = cfg[5]; P.step_tol = cfg[6];
+  P.regularize = (int)cfg[7];
+  P.max_iters = (int)cfg[8];
+  P.goal_stride = goal_stride;
+  return P;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Full SQP for B problems (OpenMP over problems when nthreads > 1).
+int i7m_cpu_solve(const double* model_packed, int N, const double* cfg, int B, const double* xu_in,
+                  const double* xcur, const double* goals, int goal_stride, const double* fext, double* xu_out,
+                  int* qp_iters, double* alphas, double* steps, int nthreads) {
+  if (N < 2 || N > 64 || B < 0) return -1;
+  const Model M = make_model(model_packed);
+  const Params P = make_params(N, cfg, goal_stride);
+  const int T = 18 * N - 6;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int b = 0; b < B; ++b) {
+    Solver<double> S(M, P);
+    double* X = xu_out + (size_t)b * T;
+    std::memcpy(X, xu_in + (size_t)b * T, sizeof(double) * T);
+    int na, ns;
+    qp_iters[b] = S.sqp(X, xcur + 12 * (size_t)b, goals + (size_t)b * N * goal_stride, fext ? fext + 6 * (size_t)b : nullptr,
+                        alphas + 8 * (size_t)b, steps + 8 * (size_t)b, &na, &ns);
+  }
+  return 0;
+}
+
+// Instrumented flop count of one SQP solve, split by stage:
+// out[0] linearise, out[1] QP (Riccati), out[2] line search (all merit evals actually run),
+// out[3] step/update; out[4] number of SQP iterations; out[5] merit evaluations.
+int i7m_cpu_count_flops(const double* model_packed, int N, const double* cfg, const double* xu_in, const double* xcur,
+                        const double* goal, int goal_stride, double* out) {
+  const Model M = make_model(model_packed);
+  const Params P = make_params(N, cfg, goal_stride);
+  const int T = 18 * N - 6;
+  Solver<CountD> S(M, P);
+  std::vector<CountD> X(xu_in, xu_in + T), xs(xcur, xcur + 12), Xn(T);
+  static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
+  uint64_t f_lin = 0, f_qp = 0, f_ls = 0, f_step = 0;
+  int iters = 0, merits = 0;
+  for (int qp = 0; qp < P.max_iters; ++qp) {
+    ++iters;
+    CountD::flops = 0;
+    S.linearize(X.data(), goal, nullptr);
+    f_lin += CountD::flops;
+    CountD::flops = 0;
+    S.riccati(X.data(), xs.data());
+    f_qp += CountD::flops;
+    CountD::flops = 0;
+    CountD base = S.merit(X.data(), X.data(), goal, nullptr);
+    ++merits;
+    double alpha = 0.0;
+    for (int ai = 0; ai < 8; ++ai) {
+      for (int e = 0; e < T; ++e) Xn[e] = X[e] + CountD(AL[ai]) * (S.sol[e] - X[e]);
+      ++merits;
+      if (S.merit(Xn.data(), X.data(), goal, nullptr) <= base) {
+        alpha = AL[ai];
+        break;
+      }
+    }
+    f_ls += CountD::flops;
+    if (alpha == 0.0) continue;
+    CountD::flops = 0;
+    CountD ss(0.0);
+    for (int e = 0; e < T; ++e) {
+      CountD stp = CountD(alpha) * (S.sol[e] - X[e]);
+      X[e] = X[e] + stp;
+      ss = ss + stp * stp;
+    }
+    double stepsize = std::sqrt(ss.v);
+    f_step += CountD::flops;
+    if (stepsize < P.step_tol) break;
+  }
+  out[0] = (double)f_lin;
+  out[1] = (double)f_qp;
+  out[2] = (double)f_ls;
+  out[3] = (double)f_step;
+  out[4] = iters;
+  out[5] = merits;
+  return 0;
+}
+
+}  // extern "C"

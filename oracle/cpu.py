@@ -1,0 +1,87 @@
+"""ORACLE (test/bench infrastructure only) — ctypes wrapper of oracle/build/libi7m_cpu.so,
+the C++ CPU restatement (oracle/cpp/i7m_cpu.cpp).  Used by tests/ (cross-check) and by
+bench.py's cpu_baseline leg and flop count.  Never imported by indy7_mpc_amd."""
+import ctypes as C
+import os
+
+import numpy as np
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libi7m_cpu.so")
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int)
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle/cpp`")
+        _lib = C.CDLL(LIB)
+        _lib.i7m_cpu_solve.argtypes = [_DP, C.c_int, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP, _DP, _DP,
+                                       C.c_int]
+        _lib.i7m_cpu_count_flops.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, C.c_int, _DP]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_DP)
+
+
+def _cfg(dt=0.01, dQ=0.01, R=1e-5, QN=100.0, eps=1.0, mu=10.0, step_tol=1e-3, regularize=True, max_iters=2):
+    return np.array([dt, dQ, R, QN, eps, mu, step_tol, float(regularize), float(max_iters)])
+
+
+def model_packed():
+    import json
+    from . import rbd
+    with open(rbd.PARAMS_PATH) as f:
+        p = json.load(f)
+    out = []
+    for j in range(6):
+        out += list(np.asarray(p["placement_R"][j], float).reshape(9))
+    for j in range(6):
+        out += list(p["placement_t"][j])
+    out += list(p["mass"])
+    for j in range(6):
+        out += list(p["com"][j])
+    for j in range(6):
+        I = np.asarray(p["inertia_com"][j], float)
+        out += [I[0, 0], I[0, 1], I[0, 2], I[1, 1], I[1, 2], I[2, 2]]
+    out += list(p.get("gravity", [0, 0, -9.81]))
+    out += list(p["q_lower"]) + list(p["q_upper"]) + list(p["v_limit"]) + list(p["effort_limit"])
+    return np.asarray(out, dtype=np.float64)
+
+
+def solve(xcur, goals, XU, N, nthreads=1, fext=None, **cfg):
+    lib = load()
+    XU = np.ascontiguousarray(XU, float)
+    B = XU.shape[0]
+    xcur = np.ascontiguousarray(xcur, float)
+    goals = np.ascontiguousarray(goals, float)
+    stride = goals.shape[1] // N
+    out = np.empty_like(XU)
+    qp = np.zeros(B, dtype=np.int32)
+    al = np.full((B, 8), np.nan)
+    st = np.full((B, 8), np.nan)
+    f = np.ascontiguousarray(fext, float) if fext is not None else None
+    m = model_packed()
+    c = _cfg(**cfg)
+    rc = lib.i7m_cpu_solve(_p(m), N, _p(c), B, _p(XU), _p(xcur), _p(goals), stride, _p(f) if f is not None else None,
+                           _p(out), qp.ctypes.data_as(_IP), _p(al), _p(st), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("i7m_cpu_solve failed")
+    return out, qp, al, st
+
+
+def count_flops(xcur, goals, XU, N, **cfg):
+    """Instrumented flops of one SQP solve: dict by stage."""
+    lib = load()
+    out = np.zeros(6)
+    m = model_packed()
+    c = _cfg(**cfg)
+    g = np.ascontiguousarray(goals, float)
+    lib.i7m_cpu_count_flops(_p(m), N, _p(c), _p(np.ascontiguousarray(XU, float)), _p(np.ascontiguousarray(xcur, float)),
+                            _p(g), g.shape[0] // N, _p(out))
+    return {"linearize": out[0], "qp": out[1], "linesearch": out[2], "step": out[3], "iters": out[4],
+            "merit_evals": out[5], "total": out[:4].sum()}

@@ -140,3 +140,18 @@ def test_linesearch_first_accept_semantics():
         assert merits[idx] <= base and all(m > base for m in merits[:idx])
     else:
         assert len(merits) == 8 and all(m > base for m in merits)
+
+
+@pytest.mark.parametrize("N", [16, 32, 64])
+def test_cpp_port_matches_numpy_oracle(N):
+    """oracle/cpp (the bench's CPU baseline + flop counter) == the numpy restatement."""
+    from oracle import cpu
+
+    f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
+    out, qp, al, st = cpu.solve(f["xcur"], f["goals"], f["XU"], N, nthreads=2)
+    for b in range(out.shape[0]):
+        assert np.linalg.norm(out[b] - f["sqp_out"][b]) <= 1e-9 * np.linalg.norm(f["sqp_out"][b])
+        assert qp[b] == f["qp_iters"][b]
+        np.testing.assert_array_equal(al[b][~np.isnan(al[b])], f["alphas"][b][~np.isnan(f["alphas"][b])])
+    fl = cpu.count_flops(f["xcur"][0], f["goals"][0], f["XU"][0], N)
+    assert fl["linearize"] > 0 and fl["qp"] > 0 and fl["iters"] == f["qp_iters"][0]

@@ -1,0 +1,63 @@
+"""Fold rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs) into
+profiles/pmc_traffic.json: HBM bytes per launch of each kernel, corrected as
+/opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes (FETCH_SIZE and WRITE_SIZE are in KiB;
+gfx950 FETCH_SIZE reads 1/2 of a wide coalesced read -> x2).
+
+    python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --batch 4096 --N 32 [--out profiles/pmc_traffic.json]
+Launches of the timed batch size only (grid size identifies them); median over launches of the
+first SQP iteration (all problems active) is reported.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import statistics
+
+
+def per_kernel(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        name = r["Kernel_Name"].split("(")[0].split("::")[-1]
+        grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+        vals[(name, grid)].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    f = per_kernel(a.fetch, "FETCH_SIZE")
+    w = per_kernel(a.write, "WRITE_SIZE")
+    grids = {"k_linearize": a.batch * 12 * (a.N - 1), "k_riccati": a.batch * 64, "k_linesearch": a.batch * 64}
+    try:
+        d = json.load(open(a.out))
+    except (OSError, ValueError):
+        d = {}
+    for k, g in grids.items():
+        gg = [key for key in f if key[0] == k and abs(key[1] - g) <= 256]
+        if not gg:
+            continue
+        fv = f[gg[0]]
+        wv = w.get(gg[0], [0.0])
+        # launches alternate iteration 1 / iteration 2 of each solve: take iteration-1 launches
+        f1, w1 = fv[0::2], wv[0::2]
+        fetch_b = 2.0 * 1024.0 * statistics.median(f1)
+        write_b = 1024.0 * statistics.median(w1)
+        d[f"{k}:B{a.batch}:N{a.N}"] = {"hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_corrected": fetch_b,
+                                       "write_bytes": write_b, "fetch_kib_raw_median": statistics.median(f1),
+                                       "launches": len(fv)}
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(d, open(a.out, "w"), indent=1)
+    print(json.dumps(d, indent=1))
+
+
+if __name__ == "__main__":
+    main()
