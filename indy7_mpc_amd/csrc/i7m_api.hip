@@ -15,6 +15,7 @@
 
 #include "../../include/indy7_mpc.h"
 #include "i7m_kernels.h"
+#include "i7m_linearize.h"
 
 using namespace i7m;
 
@@ -150,12 +151,11 @@ int timed(i7m_handle* h, int kid, F&& launch) {
 }
 
 int launch_linearize(i7m_handle* h, const SolveParams& P, const double* xu, const double* goals, const int* active) {
-  const long nthr = (long)P.B * 12 * (P.N - 1);
-  if (nthr == 0) return I7M_OK;
-  const int blk = 256;
-  const int grid = (int)((nthr + blk - 1) / blk);
+  const long knots = (long)P.B * P.N;
+  if (knots == 0) return I7M_OK;
+  const int grid = (int)((knots + KPW - 1) / KPW);
   return timed(h, I7M_K_LIN, [&] {
-    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(blk), 0, h->stream, h->d_model, P, xu, goals,
+    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
                        h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
   });
 }

@@ -2,11 +2,8 @@
 //
 // One SQP iteration of src/osqp_sqp.py:76-93 for B independent problems is three launches:
 //
-//   k_linearize   thread per (problem, knot, direction d<12): ABA + dual-RNEA derivative
-//                 column d of [dt*da/dq | I+dt*da/dv] (+ dt*Minv column, a); the d==0 lanes
-//                 also evaluate the cost linearisation (FK, LOCAL_WORLD_ALIGNED J, weights).
-//                 Replaces src/osqp_solver.py:70-135 (update_constraint_matrix +
-//                 update_cost_matrix).  Fully knot-parallel: B*(N-1)*12 lanes.
+//   k_linearize   (i7m_linearize.h) six lanes per knot: analytic world-frame derivatives of
+//                 the dynamics + cost linearisation.  Replaces src/osqp_solver.py:70-135.
 //   k_riccati     one wavefront per problem: exact solve of the equality-constrained QP
 //                 (the KKT system OSQP iterates on, src/osqp_solver.py:137-143) by a
 //                 backward Riccati recursion over 12x12 / 12x6 stage blocks staged in LDS
@@ -59,63 +56,6 @@ __device__ __forceinline__ void cost_knot(const DevModel& Md, const SolveParams&
   out[7] = P.dQ * w;
   out[8] = P.R * w;
   out[9] = nrm;
-}
-
-__global__ void __launch_bounds__(256) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
-                                                   const double* __restrict__ xu, const double* __restrict__ goals,
-                                                   const double* __restrict__ fext, const int* __restrict__ active,
-                                                   double* __restrict__ lin, double* __restrict__ cost) {
-  const int per = 12 * (P.N - 1);
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = (int)(gid / per);
-  if (b >= P.B) return;
-  if (active && !active[b]) return;
-  const int r = (int)(gid - (long)b * per);
-  const int k = r / 12;
-  const int d = r - 12 * k;
-  const DevModel& Md = *Mg;
-  const double* X = xu + (long)b * P.T + 18 * k;
-  double q[6], v[6], u[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) { q[i] = X[i]; v[i] = X[6 + i]; u[i] = X[12 + i]; }
-  double c[6], s[6], L[6][6], a[6];
-  sincos6(q, c, s);
-  const double* f6 = fext ? fext + 6L * b : nullptr;
-  forward_dynamics(Md, c, s, v, u, f6, L, a);
-  double col[6];
-  aba_deriv_column(Md, c, s, v, a, L, d, f6, col);
-  double* out = lin + ((long)b * (P.N - 1) + k) * LIN_STRIDE;
-  const double dt = P.dt;
-  if (d < 6) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) out[i * 6 + d] = dt * col[i];
-    // Bu = dt * Minv, column d from a unit solve; symmetric by construction
-    double e[6] = {0, 0, 0, 0, 0, 0};
-    e[d] = 1.0;
-    chol6_solve(L, e);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      if (i <= d) {
-        out[72 + i * 6 + d] = dt * e[i];
-        out[72 + d * 6 + i] = dt * e[i];
-      }
-    }
-    if (d == 0) {
-#pragma unroll
-      for (int i = 0; i < 6; ++i) out[108 + i] = a[i];
-    }
-  } else {
-    const int dd = d - 6;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) out[36 + i * 6 + dd] = (i == dd ? 1.0 : 0.0) + dt * col[i];
-  }
-  // cost linearisation: knot k by lane d==0, the terminal knot by lane (N-2, d==1)
-  if (d == 0 || (d == 1 && k == P.N - 2)) {
-    const int kc = (d == 0) ? k : P.N - 1;
-    const double* goal = goals + (long)b * P.N * P.goal_stride + (long)kc * P.goal_stride;
-    cost_knot(Md, P, xu + (long)b * P.T + 18 * kc, goal, kc,
-              cost + ((long)b * P.N + kc) * COST_STRIDE);
-  }
 }
 
 // ---------------------------------------------------------------------------------------

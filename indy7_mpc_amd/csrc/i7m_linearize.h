@@ -1,0 +1,370 @@
+// i7m_linearize.h — knot-parallel linearisation of the SQP subproblem (gfx950, fp64).
+//
+// Replaces, per knot k of every problem (reference src/osqp_solver.py:70-135):
+//   pin.computeABADerivatives + data.ddq + pin.integrate   (compute_dynamics_jacobians :70-81)
+//   FK + LOCAL_WORLD_ALIGNED Jacobian + cost weights       (update_cost_matrix :103-135)
+//
+// Algorithm: analytic O(n^2) derivatives of inverse dynamics in the WORLD frame (the
+// Carpentier-Mansard idea, restated from first principles): with S_j the world joint axes,
+// V_j, A_j body velocities/accelerations, I_j world inertias, IC_j / dIC_j / HC_j the
+// subtree sums of I_i, dI_i = V_i x* I_i - I_i V_i x (symmetric), I_i V_i, F^c the subtree
+// forces, W_k = S_k x V_k, Z_k = S_k x A_k - W_k x V_k:
+//   a_j = IC_j S_j, e_j = dIC_j S_j - S_j x* HC_j
+//   j >= k: dtau_j/dq_k = -(a_j.Z_k + e_j.W_k),          dtau_j/dv_k = e_j.S_k - 2 a_j.W_k
+//   j <  k: dtau_j/dq_k = S_j.y_k,  y_k = S_k x* F^c_k - IC_k Z_k - dIC_k W_k - W_k x* HC_k
+//           dtau_j/dv_k = S_j.z_k,  z_k = dIC_k S_k - 2 IC_k W_k + S_k x* HC_k
+//   M_jk = a_j.S_k (j >= k);  da/dx = -M^-1 dtau/dx at a = M^-1 (tau - b).
+// (Verified against complex-step RNEA to 1e-16 relative; tests/test_gpu_parity.py checks the
+// kernel against the oracle and against the independent dual-number path k_abad.)
+//
+// Lane mapping: one 64-lane wavefront = KPW knots x 6 link-lanes (lanes 60..63 idle); lane
+// (g, j) owns link j of knot g.  The serial kinematic chain (~600 flops) is recomputed by every
+// link-lane; the per-link work (world inertia, its rate, forces, subtree sums, one column of the
+// derivative matrices and of M^-1) is split across the lanes; the lanes of a knot exchange
+// per-link vectors through LDS.  The terminal knot of each problem only evaluates the cost.
+#pragma once
+
+#include "i7m_kernels.h"
+
+namespace i7m {
+
+constexpr int KPW = 10;   // knots per wavefront
+constexpr int XS = 32;    // LDS doubles per link slot
+
+// spatial helpers on 6-vectors [lin; ang]
+__device__ __forceinline__ void mcross(const double* a, const double* b, double* o) {  // a x b (motion)
+  o[0] = a[4] * b[2] - a[5] * b[1] + a[1] * b[5] - a[2] * b[4];
+  o[1] = a[5] * b[0] - a[3] * b[2] + a[2] * b[3] - a[0] * b[5];
+  o[2] = a[3] * b[1] - a[4] * b[0] + a[0] * b[4] - a[1] * b[3];
+  o[3] = a[4] * b[5] - a[5] * b[4];
+  o[4] = a[5] * b[3] - a[3] * b[5];
+  o[5] = a[3] * b[4] - a[4] * b[3];
+}
+__device__ __forceinline__ void fcross(const double* m, const double* f, double* o) {  // m x* f
+  o[0] = m[4] * f[2] - m[5] * f[1];
+  o[1] = m[5] * f[0] - m[3] * f[2];
+  o[2] = m[3] * f[1] - m[4] * f[0];
+  o[3] = m[4] * f[5] - m[5] * f[4] + m[1] * f[2] - m[2] * f[1];
+  o[4] = m[5] * f[3] - m[3] * f[5] + m[2] * f[0] - m[0] * f[2];
+  o[5] = m[3] * f[4] - m[4] * f[3] + m[0] * f[1] - m[1] * f[0];
+}
+__device__ __forceinline__ double dot6(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+// inertia (m, h[3], I[6] sym xx xy xz yy yz zz, about the world origin) times motion x
+__device__ __forceinline__ void imul(double m, const double* h, const double* I, const double* x, double* o) {
+  o[0] = m * x[0] - (h[1] * x[5] - h[2] * x[4]);
+  o[1] = m * x[1] - (h[2] * x[3] - h[0] * x[5]);
+  o[2] = m * x[2] - (h[0] * x[4] - h[1] * x[3]);
+  o[3] = I[0] * x[3] + I[1] * x[4] + I[2] * x[5] + (h[1] * x[2] - h[2] * x[1]);
+  o[4] = I[1] * x[3] + I[3] * x[4] + I[4] * x[5] + (h[2] * x[0] - h[0] * x[2]);
+  o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
+}
+
+__global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
+                                                  const double* __restrict__ xu, const double* __restrict__ goals,
+                                                  const double* __restrict__ fext, const int* __restrict__ active,
+                                                  double* __restrict__ lin, double* __restrict__ cost) {
+  const DevModel& Md = *Mg;
+  const int l = threadIdx.x;
+  const int g = l / 6;
+  const int j = l - 6 * g;
+  const long kg = (long)blockIdx.x * KPW + g;
+  const int b = (int)(kg / P.N);
+  const int k = (int)(kg - (long)b * P.N);
+  const bool valid = (g < KPW) && (b < P.B) && (!active || active[b]);
+  const bool dyn = valid && (k < P.N - 1);
+  const int gg = g < KPW ? g : 0;
+
+  __shared__ double xs[KPW][6][XS];
+  __shared__ double sM[KPW][36];
+  __shared__ double st0[KPW][6];
+
+  const double* X = xu + (long)(valid ? b : 0) * P.T + 18 * (valid ? k : 0);
+  double q[6], v[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    q[i] = X[i];
+    v[i] = (dyn ? X[6 + i] : 0.0);
+  }
+  double c[6], s[6];
+  sincos6(q, c, s);
+
+  // ---- cost linearisation (lane 0 of each knot)
+  if (valid && j == 0) {
+    const double* goal = goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride;
+    cost_knot(Md, P, X, goal, k, cost + ((long)b * P.N + k) * COST_STRIDE);
+  }
+
+  // ---- 1. serial chain (every lane): world placement of each joint, S, V, A0 (qdd = 0)
+  double Rj[9], pj[3], Sj[6], Vj[6], A0j[6];
+  {
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double p[3] = {0, 0, 0};
+    double V[6] = {0, 0, 0, 0, 0, 0};
+    double A[6] = {-Md.g[0], -Md.g[1], -Md.g[2], 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double* Rp = Md.Rp[i];
+      const double* t = Md.tp[i];
+      double np_[3], RR[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[3 * r] * t[0] + R[3 * r + 1] * t[1] + R[3 * r + 2] * t[2];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int qq = 0; qq < 3; ++qq) RR[3 * r + qq] = R[3 * r] * Rp[qq] + R[3 * r + 1] * Rp[3 + qq] + R[3 * r + 2] * Rp[6 + qq];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        R[3 * r] = RR[3 * r] * c[i] + RR[3 * r + 1] * s[i];
+        R[3 * r + 1] = RR[3 * r + 1] * c[i] - RR[3 * r] * s[i];
+        R[3 * r + 2] = RR[3 * r + 2];
+        p[r] = np_[r];
+      }
+      // S = (p x z; z), z = R[:,2]
+      double S[6];
+      S[3] = R[2]; S[4] = R[5]; S[5] = R[8];
+      S[0] = p[1] * S[5] - p[2] * S[4];
+      S[1] = p[2] * S[3] - p[0] * S[5];
+      S[2] = p[0] * S[4] - p[1] * S[3];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) V[r] += S[r] * v[i];
+      double VS[6];
+      mcross(V, S, VS);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) A[r] += VS[r] * v[i];
+      if (i == j) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) Rj[r] = R[r];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) pj[r] = p[r];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) { Sj[r] = S[r]; Vj[r] = V[r]; A0j[r] = A[r]; }
+      }
+    }
+  }
+
+  // ---- 2. own link: world inertia (m, h, Ib), its rate (hd, Ibd), momentum, bias force
+  const double m = Md.m[j];
+  double h[3], Ib[6], hV[6], F0[6], hd[3], Ibd[6];
+  {
+    const double* hl = Md.h[j];
+    const double* Io = Md.Io[j];
+    // R Io R^T
+    double Iof[9] = {Io[0], Io[1], Io[2], Io[1], Io[3], Io[4], Io[2], Io[4], Io[5]};
+    double RI[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int qq = 0; qq < 3; ++qq) RI[3 * r + qq] = Rj[3 * r] * Iof[qq] + Rj[3 * r + 1] * Iof[3 + qq] + Rj[3 * r + 2] * Iof[6 + qq];
+    double hr[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) hr[r] = Rj[3 * r] * hl[0] + Rj[3 * r + 1] * hl[1] + Rj[3 * r + 2] * hl[2];
+    const double* t = pj;
+    const double ht = hr[0] * t[0] + hr[1] * t[1] + hr[2] * t[2];
+    const double tt = t[0] * t[0] + t[1] * t[1] + t[2] * t[2];
+    const double dg = 2.0 * ht + m * tt;
+    const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int r = iu[e][0], qq = iu[e][1];
+      double val = RI[3 * r] * Rj[3 * qq] + RI[3 * r + 1] * Rj[3 * qq + 1] + RI[3 * r + 2] * Rj[3 * qq + 2];
+      val -= (t[r] * hr[qq] + hr[r] * t[qq]) + m * t[r] * t[qq];
+      if (r == qq) val += dg;
+      Ib[e] = val;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) h[r] = hr[r] + m * t[r];
+    imul(m, h, Ib, Vj, hV);
+    double IA[6], VxH[6];
+    imul(m, h, Ib, A0j, IA);
+    fcross(Vj, hV, VxH);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) F0[r] = IA[r] + VxH[r];
+    if (fext && j == 5 && valid) {
+      // local joint-6 wrench -> world: f_w = R f, n_w = R n + p x f_w
+      const double* fe = fext + 6L * b;
+      double fw[3], nw[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        fw[r] = Rj[3 * r] * fe[0] + Rj[3 * r + 1] * fe[1] + Rj[3 * r + 2] * fe[2];
+        nw[r] = Rj[3 * r] * fe[3] + Rj[3 * r + 1] * fe[4] + Rj[3 * r + 2] * fe[5];
+      }
+      F0[0] -= fw[0]; F0[1] -= fw[1]; F0[2] -= fw[2];
+      F0[3] -= nw[0] + (pj[1] * fw[2] - pj[2] * fw[1]);
+      F0[4] -= nw[1] + (pj[2] * fw[0] - pj[0] * fw[2]);
+      F0[5] -= nw[2] + (pj[0] * fw[1] - pj[1] * fw[0]);
+    }
+    // rate: hd = m v + w x h ; Ibd = [w]x Ib - Ib [w]x - h v^T - v h^T + 2 (v.h) I
+    const double* vl = Vj;
+    const double* w = Vj + 3;
+    hd[0] = m * vl[0] + (w[1] * h[2] - w[2] * h[1]);
+    hd[1] = m * vl[1] + (w[2] * h[0] - w[0] * h[2]);
+    hd[2] = m * vl[2] + (w[0] * h[1] - w[1] * h[0]);
+    double Ibf[9] = {Ib[0], Ib[1], Ib[2], Ib[1], Ib[3], Ib[4], Ib[2], Ib[4], Ib[5]};
+    double WI[9];  // [w]x Ib
+#pragma unroll
+    for (int qq = 0; qq < 3; ++qq) {
+      WI[qq] = w[1] * Ibf[6 + qq] - w[2] * Ibf[3 + qq];
+      WI[3 + qq] = w[2] * Ibf[qq] - w[0] * Ibf[6 + qq];
+      WI[6 + qq] = w[0] * Ibf[3 + qq] - w[1] * Ibf[qq];
+    }
+    const double vh = vl[0] * h[0] + vl[1] * h[1] + vl[2] * h[2];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int r = iu[e][0], qq = iu[e][1];
+      // ([w]x Ib - Ib [w]x)_{r,qq} = WI[r][qq] + WI[qq][r]  (Ib symmetric)
+      double val = WI[3 * r + qq] + WI[3 * qq + r] - (h[r] * vl[qq] + vl[r] * h[qq]);
+      if (r == qq) val += 2.0 * vh;
+      Ibd[e] = val;
+    }
+  }
+  // publish: [0]m [1..3]h [4..9]Ib [10..12]hd [13..18]Ibd [19..24]hV [25..30]F0
+  double* my = &xs[gg][j][0];
+  if (g < KPW) {
+    my[0] = m;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) { my[1 + r] = h[r]; my[10 + r] = hd[r]; }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { my[4 + r] = Ib[r]; my[13 + r] = Ibd[r]; my[19 + r] = hV[r]; my[25 + r] = F0[r]; }
+  }
+  __syncthreads();
+
+  // ---- 3. subtree sums for link j
+  double cm = 0, ch[3] = {0, 0, 0}, cI[6] = {0, 0, 0, 0, 0, 0}, chd[3] = {0, 0, 0}, cId[6] = {0, 0, 0, 0, 0, 0};
+  double HC[6] = {0, 0, 0, 0, 0, 0}, Fc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (i >= j) {
+      const double* o = &xs[gg][i][0];
+      cm += o[0];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { ch[r] += o[1 + r]; chd[r] += o[10 + r]; }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) { cI[r] += o[4 + r]; cId[r] += o[13 + r]; HC[r] += o[19 + r]; Fc[r] += o[25 + r]; }
+    }
+  }
+  const double tau0 = dot6(Sj, Fc);
+  double aj[6], ej[6];
+  imul(cm, ch, cI, Sj, aj);
+  {
+    double bj[6], cj[6];
+    imul(0.0, chd, cId, Sj, bj);
+    fcross(Sj, HC, cj);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ej[r] = bj[r] - cj[r];
+  }
+  __syncthreads();  // everyone has read the phase-1 slots
+  // publish a_j, e_j, S_j for the M row and the derivative columns
+  if (g < KPW) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { my[r] = aj[r]; my[6 + r] = ej[r]; my[12 + r] = Sj[r]; }
+    st0[gg][j] = tau0;
+  }
+  __syncthreads();
+  // M row j: M_jk = a_j . S_k (k <= j)
+  if (g < KPW) {
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      if (kk <= j) {
+        const double mv = dot6(aj, &xs[gg][kk][12]);
+        sM[gg][6 * j + kk] = mv;
+        sM[gg][6 * kk + j] = mv;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 4. a = M^-1 (u - tau0) (every lane), dA_j = sum_{i<=j} S_i a_i, g_j = I_j dA_j
+  double L[6][6], acc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) L[r][cc] = sM[gg][6 * r + cc];
+  chol6(L);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) acc[r] = (dyn ? X[12 + r] : 0.0) - st0[gg][r];
+  chol6_solve(L, acc);
+  double dA[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (i <= j) {
+      const double* Si = &xs[gg][i][12];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) dA[r] += Si[r] * acc[i];
+    }
+  }
+  double gI[6];
+  imul(m, h, Ib, dA, gI);
+  if (g < KPW) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) my[18 + r] = gI[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (i >= j) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) Fc[r] += xs[gg][i][18 + r];
+    }
+  }
+  // ---- 5. W, Z, y, z of link j
+  double Wj[6], Zj[6], yj[6], zj[6];
+  {
+    double Aj[6], t1[6], t2[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) Aj[r] = A0j[r] + dA[r];
+    mcross(Sj, Vj, Wj);
+    mcross(Sj, Aj, t1);
+    mcross(Wj, Vj, t2);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) Zj[r] = t1[r] - t2[r];
+    double a1[6], a2[6], a3[6], a4[6];
+    fcross(Sj, Fc, a1);
+    imul(cm, ch, cI, Zj, a2);
+    imul(0.0, chd, cId, Wj, a3);
+    fcross(Wj, HC, a4);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) yj[r] = a1[r] - a2[r] - a3[r] - a4[r];
+    double b1[6], b2[6], b3[6];
+    imul(0.0, chd, cId, Sj, b1);
+    imul(cm, ch, cI, Wj, b2);
+    fcross(Sj, HC, b3);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) zj[r] = b1[r] - 2.0 * b2[r] + b3[r];
+  }
+  // ---- 6. column j of dtau/dq, dtau/dv, then -M^-1 and outputs
+  double dq[6], dv[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const double* o = &xs[gg][r][0];
+    if (r >= j) {
+      dq[r] = -(dot6(o, Zj) + dot6(o + 6, Wj));
+      dv[r] = dot6(o + 6, Sj) - 2.0 * dot6(o, Wj);
+    } else {
+      dq[r] = dot6(o + 12, yj);
+      dv[r] = dot6(o + 12, zj);
+    }
+  }
+  chol6_solve(L, dq);
+  chol6_solve(L, dv);
+  double em[6] = {0, 0, 0, 0, 0, 0};
+  em[j] = 1.0;
+  chol6_solve(L, em);
+  if (dyn) {
+    double* out = lin + ((long)b * (P.N - 1) + k) * LIN_STRIDE;
+    const double dt = P.dt;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      out[6 * r + j] = -dt * dq[r];
+      out[36 + 6 * r + j] = (r == j ? 1.0 : 0.0) - dt * dv[r];
+      if (r <= j) {
+        out[72 + 6 * r + j] = dt * em[r];
+        out[72 + 6 * j + r] = dt * em[r];
+      }
+    }
+    out[108 + j] = acc[j];
+  }
+}
+
+}  // namespace i7m

@@ -101,3 +101,26 @@ def test_full_sqp_matches_oracle(lib, model, N, B):
         np.testing.assert_array_equal(st["alphas"][b][:na], s["linesearch_alphas"]["values"])
         rel = np.linalg.norm(out[b] - ref) / np.linalg.norm(ref)
         assert rel < 1e-6, (b, rel)
+
+
+def test_analytic_linearisation_equals_dual_number_path(lib, model):
+    """Two independent device derivative algorithms agree: k_linearize (analytic world-frame
+    O(n^2)) vs k_abad (forward-mode dual-number RNEA), on the same knots."""
+    N, B = 32, 5
+    xcur, goals, XU = synthetic_batch(B, N, seed=17)
+    XU = XU + np.random.default_rng(4).normal(0, 0.8, XU.shape)
+    h = _handle(lib, model, N, B)
+    lin, cost = h.linearize(XU, goals)
+    X = XU.reshape(B, -1)
+    idx = [(b, k) for b in range(B) for k in range(N - 1)]
+    q = np.array([X[b, 18 * k:18 * k + 6] for b, k in idx])
+    v = np.array([X[b, 18 * k + 6:18 * k + 12] for b, k in idx])
+    u = np.array([X[b, 18 * k + 12:18 * k + 18] for b, k in idx])
+    dq, dv, Mi, a = h.aba_derivatives(q, v, u)
+    L = lin.reshape(-1, 114)
+    dt = 0.01
+    for n in range(len(idx)):
+        np.testing.assert_allclose(L[n, :36].reshape(6, 6), dt * dq[n], rtol=1e-9, atol=1e-10 * max(1, dt * np.abs(dq[n]).max()))
+        np.testing.assert_allclose(L[n, 36:72].reshape(6, 6), np.eye(6) + dt * dv[n], rtol=1e-9, atol=1e-11)
+        np.testing.assert_allclose(L[n, 72:108].reshape(6, 6), dt * Mi[n], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(L[n, 108:], a[n], rtol=1e-9, atol=1e-9)
