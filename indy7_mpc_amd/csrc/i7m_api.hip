@@ -16,6 +16,7 @@
 #include "../../include/indy7_mpc.h"
 #include "i7m_kernels.h"
 #include "i7m_linearize.h"
+#include "i7m_riccati.h"
 
 using namespace i7m;
 
@@ -55,6 +56,7 @@ struct i7m_handle {
   int* d_active = nullptr;
   ProblemStats* d_stats = nullptr;
   double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
+  uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
   bool has_fext = false;
   size_t goal_cap = 0;
   // timing
@@ -164,8 +166,8 @@ int launch_riccati(i7m_handle* h, const SolveParams& P, const double* xu, const 
                    double* sol) {
   if (P.B == 0) return I7M_OK;
   return timed(h, I7M_K_RICCATI, [&] {
-    hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost, active,
-                       h->d_kbuf, sol);
+    hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, h->d_ric_desc, xu, xs, h->d_lin, h->d_cost,
+                       active, h->d_kbuf, sol);
   });
 }
 
@@ -283,8 +285,12 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_kbuf, Bm * (N - 1) * KBUF_STRIDE * 8) && alloc((void**)&h->d_aux, scratch * 8) &&
             alloc((void**)&h->d_out, scratch * 8) &&
             alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
-            alloc((void**)&h->d_fext, Bm * 6 * 8);
+            alloc((void**)&h->d_fext, Bm * 6 * 8) && alloc((void**)&h->d_ric_desc, RIC_DESC_WORDS * 4);
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
+  std::vector<uint32_t> desc(RIC_DESC_WORDS);
+  build_riccati_desc(desc.data());
+  if (hipMemcpy(h->d_ric_desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return bail(fail(I7M_EHIP, "descriptor upload failed"));
   DevModel dm = make_dev_model(cfg->model);
   if (hipMemcpy(h->d_model, &dm, sizeof(dm), hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(I7M_EHIP, "model upload failed"));
@@ -297,7 +303,7 @@ void i7m_destroy(i7m_handle* h) {
   hipSetDevice(h->dev);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext};
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& t : h->ev) {

@@ -4,10 +4,8 @@
 //
 //   k_linearize   (i7m_linearize.h) six lanes per knot: analytic world-frame derivatives of
 //                 the dynamics + cost linearisation.  Replaces src/osqp_solver.py:70-135.
-//   k_riccati     one wavefront per problem: exact solve of the equality-constrained QP
-//                 (the KKT system OSQP iterates on, src/osqp_solver.py:137-143) by a
-//                 backward Riccati recursion over 12x12 / 12x6 stage blocks staged in LDS
-//                 and a forward rollout.  Writes sol.x.
+//   k_riccati     (i7m_riccati.h) one wavefront per problem: exact solve of the
+//                 equality-constrained QP (src/osqp_solver.py:137-143), Riccati recursion.
 //   k_linesearch  one wavefront per problem, lanes = (candidate alpha, knot): merit of the
 //                 base point and of the backtracking alphas, several candidates per round,
 //                 first-accept rule of src/osqp_sqp.py:58-72, then the SQP step, step-size
@@ -56,249 +54,6 @@ __device__ __forceinline__ void cost_knot(const DevModel& Md, const SolveParams&
   out[7] = P.dQ * w;
   out[8] = P.R * w;
   out[9] = nrm;
-}
-
-// ---------------------------------------------------------------------------------------
-// Riccati: one 64-lane wavefront (= workgroup) per problem.
-__global__ void __launch_bounds__(64) k_riccati(SolveParams P, const double* __restrict__ xu,
-                                                const double* __restrict__ xs, const double* __restrict__ lin,
-                                                const double* __restrict__ cost, const int* __restrict__ active,
-                                                double* __restrict__ kbuf, double* __restrict__ sol) {
-  const int b = blockIdx.x;
-  if (b >= P.B) return;
-  if (active && !active[b]) return;
-  const int l = threadIdx.x;
-  const int N = P.N;
-  const double dt = P.dt;
-  __shared__ double sV[144], sv[12], sVA[144], sT[36], ss[12], sG[72], sH[36], sh[6], svA[12], sK[78];
-  __shared__ double sAq[36], sAv[36], sBu[36], sa[6], sc[6], sw[COST_STRIDE], sX[18];
-  const double* X = xu + (long)b * P.T;
-  const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
-  const double* CB = cost + (long)b * N * COST_STRIDE;
-  double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
-
-  // ---- terminal cost-to-go: V = P_{N-1}, v = g_{N-1}
-  if (l < COST_STRIDE) sw[l] = CB[(N - 1) * COST_STRIDE + l];
-  __syncthreads();
-  for (int e = l; e < 144; e += 64) {
-    const int r = e / 12, cc = e - 12 * (e / 12);
-    double val = 0.0;
-    if (r < 6 && cc < 6) val = sw[6] * (sw[r] * sw[cc]);
-    else if (r == cc) val = sw[7];
-    sV[e] = val;
-  }
-  if (l < 12) sv[l] = (l < 6) ? sw[6] * sw[l] : sw[7] * X[18 * (N - 1) + l];
-  __syncthreads();
-
-  // prefetch registers: stage data = lin (114) + cost (10) + XU_k (18) = 142 values
-  double pf0, pf1, pf2;
-  auto fetch = [&](int k, double& a0, double& a1, double& a2) {
-    const int e0 = l, e1 = l + 64, e2 = l + 128;
-    auto get = [&](int e) -> double {
-      if (e < LIN_STRIDE) return LINb[(long)k * LIN_STRIDE + e];
-      if (e < LIN_STRIDE + COST_STRIDE) return CB[k * COST_STRIDE + (e - LIN_STRIDE)];
-      if (e < LIN_STRIDE + COST_STRIDE + 18) return X[18 * k + (e - LIN_STRIDE - COST_STRIDE)];
-      return 0.0;
-    };
-    a0 = get(e0); a1 = get(e1); a2 = get(e2);
-  };
-  auto stash = [&](double a0, double a1, double a2) {
-    auto put = [&](int e, double val) {
-      if (e < 36) sAq[e] = val;
-      else if (e < 72) sAv[e - 36] = val;
-      else if (e < 108) sBu[e - 72] = val;
-      else if (e < 114) sa[e - 108] = val;
-      else if (e < 124) sw[e - 114] = val;
-      else if (e < 142) sX[e - 124] = val;
-    };
-    put(l, a0); put(l + 64, a1); put(l + 128, a2);
-  };
-  fetch(N - 2, pf0, pf1, pf2);
-
-  for (int k = N - 2; k >= 0; --k) {
-    stash(pf0, pf1, pf2);
-    __syncthreads();
-    if (k > 0) fetch(k - 1, pf0, pf1, pf2);
-    // c_v = v + dt a - (Aq q + Av v + Bu u)    (src/osqp_solver.py:76-81)
-    if (l < 6) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) acc += sAq[l * 6 + j] * sX[j] + sAv[l * 6 + j] * sX[6 + j] + sBu[l * 6 + j] * sX[12 + j];
-      sc[l] = (sX[6 + l] + sa[l] * dt) - acc;
-    }
-    __syncthreads();
-    // ---- step A: VA = V A (144), T = Vvv Bu (36), s = v + V c (12)
-    for (int e = l; e < 192; e += 64) {
-      if (e < 144) {
-        const int r = e / 12, cc = e - 12 * (e / 12);
-        double acc;
-        if (cc < 6) {
-          acc = sV[r * 12 + cc];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sAq[m * 6 + cc];
-        } else {
-          const int c2 = cc - 6;
-          acc = dt * sV[r * 12 + c2];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sAv[m * 6 + c2];
-        }
-        sVA[e] = acc;
-      } else if (e < 180) {
-        const int t = e - 144, r = t / 6, cc = t - 6 * (t / 6);
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sV[(6 + r) * 12 + 6 + m] * sBu[m * 6 + cc];
-        sT[t] = acc;
-      } else {
-        const int r = e - 180;
-        double acc = sv[r];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sV[r * 12 + 6 + m] * sc[m];
-        ss[r] = acc;
-      }
-    }
-    __syncthreads();
-    // ---- step B: AtVA (upper 78) -> sV, G (72), H (21 upper), h (6), vA (12)
-    for (int e = l; e < 189; e += 64) {
-      if (e < 78) {
-        // upper-triangular index e -> (r, cc), r <= cc
-        int r = 0, rem = e;
-        while (rem >= 12 - r) { rem -= 12 - r; ++r; }
-        const int cc = r + rem;
-        double acc;
-        if (r < 6) {
-          acc = sVA[r * 12 + cc];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sAq[m * 6 + r] * sVA[(6 + m) * 12 + cc];
-        } else {
-          const int r2 = r - 6;
-          acc = dt * sVA[r2 * 12 + cc];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sAv[m * 6 + r2] * sVA[(6 + m) * 12 + cc];
-        }
-        sV[r * 12 + cc] = acc;
-        sV[cc * 12 + r] = acc;
-      } else if (e < 150) {
-        const int t = e - 78, r = t / 12, cc = t - 12 * (t / 12);
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * sVA[(6 + m) * 12 + cc];
-        sG[t] = acc;
-      } else if (e < 171) {
-        int t = e - 150, r = 0;
-        while (t >= 6 - r) { t -= 6 - r; ++r; }
-        const int cc = r + t;
-        double acc = (r == cc) ? sw[8] : 0.0;
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * sT[m * 6 + cc];
-        sH[r * 6 + cc] = acc;
-        sH[cc * 6 + r] = acc;
-      } else if (e < 177) {
-        const int r = e - 171;
-        double acc = sw[8] * sX[12 + r];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sBu[m * 6 + r] * ss[6 + m];
-        sh[r] = acc;
-      } else {
-        const int r = e - 177;
-        double acc;
-        if (r < 6) {
-          acc = sw[6] * sw[r] + ss[r];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sAq[m * 6 + r] * ss[6 + m];
-        } else {
-          const int r2 = r - 6;
-          acc = sw[7] * sX[6 + r2] + dt * ss[r2];
-#pragma unroll
-          for (int m = 0; m < 6; ++m) acc += sAv[m * 6 + r2] * ss[6 + m];
-        }
-        svA[r] = acc;
-      }
-    }
-    __syncthreads();
-    // ---- step C: [K | kff] = -H^-1 [G | h]   (13 right-hand sides, one per lane)
-    if (l < 13) {
-      double Lh[6][6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Lh[i][j] = sH[i * 6 + j];
-      chol6(Lh);
-      double rhs[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) rhs[i] = (l < 12) ? sG[i * 12 + l] : sh[i];
-      chol6_solve(Lh, rhs);
-      if (l < 12) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) sK[i * 12 + l] = -rhs[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) sK[72 + i] = -rhs[i];
-      }
-    }
-    __syncthreads();
-    // ---- step D: V = Q + AtVA + G^T K (upper 78), v = q + A^T s + G^T kff ; store K, kff, c_v
-    for (int e = l; e < 90; e += 64) {
-      if (e < 78) {
-        int r = 0, rem = e;
-        while (rem >= 12 - r) { rem -= 12 - r; ++r; }
-        const int cc = r + rem;
-        double acc = sV[r * 12 + cc];
-        if (r < 6 && cc < 6) acc += sw[6] * (sw[r] * sw[cc]);
-        else if (r == cc) acc += sw[7];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sG[m * 12 + r] * sK[m * 12 + cc];
-        sV[r * 12 + cc] = acc;
-        sV[cc * 12 + r] = acc;
-      } else {
-        const int r = e - 78;
-        double acc = svA[r];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) acc += sG[m * 12 + r] * sK[72 + m];
-        sv[r] = acc;
-      }
-    }
-    for (int e = l; e < KBUF_STRIDE; e += 64) KB[(long)k * KBUF_STRIDE + e] = (e < 78) ? sK[e] : sc[e - 78];
-    __syncthreads();
-  }
-
-  // ---- forward rollout: x_0 = xs; u_k = K x_k + kff; x_{k+1} = A x + B u + c
-  double* S = sol + (long)b * P.T;
-  __shared__ double sx[2][12], su[6];
-  if (l < 12) {
-    const double x0 = xs[(long)b * 12 + l];
-    sx[0][l] = x0;
-    S[l] = x0;
-  }
-  __syncthreads();
-  for (int k = 0; k < N - 1; ++k) {
-    const int cur = k & 1;
-    if (l < 6) {
-      const double* Kk = KB + (long)k * KBUF_STRIDE;
-      double acc = Kk[72 + l];
-#pragma unroll
-      for (int j = 0; j < 12; ++j) acc += Kk[l * 12 + j] * sx[cur][j];
-      su[l] = acc;
-      S[18 * k + 12 + l] = acc;
-    }
-    __syncthreads();
-    if (l < 12) {
-      double nx;
-      if (l < 6) {
-        nx = sx[cur][l] + dt * sx[cur][6 + l];
-      } else {
-        const int i = l - 6;
-        const double* Lk = LINb + (long)k * LIN_STRIDE;
-        double acc = KB[(long)k * KBUF_STRIDE + 78 + i];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) acc += Lk[i * 6 + j] * sx[cur][j] + Lk[36 + i * 6 + j] * sx[cur][6 + j] + Lk[72 + i * 6 + j] * su[j];
-        nx = acc;
-      }
-      sx[cur ^ 1][l] = nx;
-      S[18 * (k + 1) + l] = nx;
-    }
-    __syncthreads();
-  }
 }
 
 // ---------------------------------------------------------------------------------------
