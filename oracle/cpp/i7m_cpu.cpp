@@ -325,38 +325,223 @@ struct Solver {
     sol.resize(T);
   }
 
+  // Analytic world-frame O(n^2) derivatives (the algorithm of the GPU's k_linearize,
+  // indy7_mpc_amd/csrc/i7m_linearize.h), executed once per knot.
+  static void mcross(const R* a, const R* b, R* o) {
+    o[0] = a[4] * b[2] - a[5] * b[1] + a[1] * b[5] - a[2] * b[4];
+    o[1] = a[5] * b[0] - a[3] * b[2] + a[2] * b[3] - a[0] * b[5];
+    o[2] = a[3] * b[1] - a[4] * b[0] + a[0] * b[4] - a[1] * b[3];
+    o[3] = a[4] * b[5] - a[5] * b[4];
+    o[4] = a[5] * b[3] - a[3] * b[5];
+    o[5] = a[3] * b[4] - a[4] * b[3];
+  }
+  static void fcross(const R* m, const R* f, R* o) {
+    o[0] = m[4] * f[2] - m[5] * f[1];
+    o[1] = m[5] * f[0] - m[3] * f[2];
+    o[2] = m[3] * f[1] - m[4] * f[0];
+    o[3] = m[4] * f[5] - m[5] * f[4] + m[1] * f[2] - m[2] * f[1];
+    o[4] = m[5] * f[3] - m[3] * f[5] + m[2] * f[0] - m[0] * f[2];
+    o[5] = m[3] * f[4] - m[4] * f[3] + m[0] * f[1] - m[1] * f[0];
+  }
+  static R dot6(const R* a, const R* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5]; }
+  static void imul(R m, const R* h, const R* I, const R* x, R* o) {
+    o[0] = m * x[0] - (h[1] * x[5] - h[2] * x[4]);
+    o[1] = m * x[1] - (h[2] * x[3] - h[0] * x[5]);
+    o[2] = m * x[2] - (h[0] * x[4] - h[1] * x[3]);
+    o[3] = I[0] * x[3] + I[1] * x[4] + I[2] * x[5] + (h[1] * x[2] - h[2] * x[1]);
+    o[4] = I[1] * x[3] + I[3] * x[4] + I[4] * x[5] + (h[2] * x[0] - h[0] * x[2]);
+    o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
+  }
+  static void imul0(const R* h, const R* I, const R* x, R* o) {  // rate form: zero mass
+    o[0] = R(0) - (h[1] * x[5] - h[2] * x[4]);
+    o[1] = R(0) - (h[2] * x[3] - h[0] * x[5]);
+    o[2] = R(0) - (h[0] * x[4] - h[1] * x[3]);
+    o[3] = I[0] * x[3] + I[1] * x[4] + I[2] * x[5] + (h[1] * x[2] - h[2] * x[1]);
+    o[4] = I[1] * x[3] + I[3] * x[4] + I[4] * x[5] + (h[2] * x[0] - h[0] * x[2]);
+    o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
+  }
+
   void linearize(const R* X, const double* goal, const double* f6) {
     const R dt = R(P.dt);
+    static const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
     for (int k = 0; k < P.N - 1; ++k) {
       const R* x = X + 18 * k;
-      R c[6], s[6], L[6][6], a[6];
+      const R* v = x + 6;
+      R c[6], s[6];
       for (int i = 0; i < 6; ++i) sincos2(x[i], &s[i], &c[i]);
-      forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
+      R Rw[6][9], pw[6][3], S[6][6], V[6][6], A0[6][6];
+      {
+        R Rc[9] = {R(1), R(0), R(0), R(0), R(1), R(0), R(0), R(0), R(1)}, pc[3] = {R(0), R(0), R(0)};
+        R Vc[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+        R Ac[6] = {R(-Md.g[0]), R(-Md.g[1]), R(-Md.g[2]), R(0), R(0), R(0)};
+        for (int i = 0; i < 6; ++i) {
+          const double* Rp = Md.Rp[i];
+          const double* t = Md.tp[i];
+          R np_[3], RR[9];
+          for (int r = 0; r < 3; ++r) np_[r] = pc[r] + Rc[3 * r] * R(t[0]) + Rc[3 * r + 1] * R(t[1]) + Rc[3 * r + 2] * R(t[2]);
+          for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q) RR[3 * r + q] = Rc[3 * r] * R(Rp[q]) + Rc[3 * r + 1] * R(Rp[3 + q]) + Rc[3 * r + 2] * R(Rp[6 + q]);
+          for (int r = 0; r < 3; ++r) {
+            Rc[3 * r] = RR[3 * r] * c[i] + RR[3 * r + 1] * s[i];
+            Rc[3 * r + 1] = RR[3 * r + 1] * c[i] - RR[3 * r] * s[i];
+            Rc[3 * r + 2] = RR[3 * r + 2];
+            pc[r] = np_[r];
+          }
+          R* Si = S[i];
+          Si[3] = Rc[2]; Si[4] = Rc[5]; Si[5] = Rc[8];
+          Si[0] = pc[1] * Si[5] - pc[2] * Si[4];
+          Si[1] = pc[2] * Si[3] - pc[0] * Si[5];
+          Si[2] = pc[0] * Si[4] - pc[1] * Si[3];
+          for (int r = 0; r < 6; ++r) Vc[r] = Vc[r] + Si[r] * v[i];
+          R VS[6];
+          mcross(Vc, Si, VS);
+          for (int r = 0; r < 6; ++r) Ac[r] = Ac[r] + VS[r] * v[i];
+          for (int r = 0; r < 9; ++r) Rw[i][r] = Rc[r];
+          for (int r = 0; r < 3; ++r) pw[i][r] = pc[r];
+          for (int r = 0; r < 6; ++r) { V[i][r] = Vc[r]; A0[i][r] = Ac[r]; }
+        }
+      }
+      // per link: world inertia, rate, momentum, bias force
+      R m_[6], h[6][3], Ib[6][6], hd[6][3], Ibd[6][6], hV[6][6], F0[6][6];
+      for (int i = 0; i < 6; ++i) {
+        const R m = R(Md.m[i]);
+        const double* hl = Md.h[i];
+        const double* Io = Md.Io[i];
+        const R* Rj = Rw[i];
+        const R* t = pw[i];
+        R Iof[9] = {R(Io[0]), R(Io[1]), R(Io[2]), R(Io[1]), R(Io[3]), R(Io[4]), R(Io[2]), R(Io[4]), R(Io[5])};
+        R RI[9], hr[3];
+        for (int r = 0; r < 3; ++r)
+          for (int q = 0; q < 3; ++q) RI[3 * r + q] = Rj[3 * r] * Iof[q] + Rj[3 * r + 1] * Iof[3 + q] + Rj[3 * r + 2] * Iof[6 + q];
+        for (int r = 0; r < 3; ++r) hr[r] = Rj[3 * r] * R(hl[0]) + Rj[3 * r + 1] * R(hl[1]) + Rj[3 * r + 2] * R(hl[2]);
+        const R ht = hr[0] * t[0] + hr[1] * t[1] + hr[2] * t[2];
+        const R tt = t[0] * t[0] + t[1] * t[1] + t[2] * t[2];
+        const R dg = R(2.0) * ht + m * tt;
+        for (int e = 0; e < 6; ++e) {
+          const int r = iu[e][0], q = iu[e][1];
+          R val = RI[3 * r] * Rj[3 * q] + RI[3 * r + 1] * Rj[3 * q + 1] + RI[3 * r + 2] * Rj[3 * q + 2];
+          val = val - ((t[r] * hr[q] + hr[r] * t[q]) + m * t[r] * t[q]);
+          if (r == q) val = val + dg;
+          Ib[i][e] = val;
+        }
+        for (int r = 0; r < 3; ++r) h[i][r] = hr[r] + m * t[r];
+        m_[i] = m;
+        imul(m, h[i], Ib[i], V[i], hV[i]);
+        R IA[6], VxH[6];
+        imul(m, h[i], Ib[i], A0[i], IA);
+        fcross(V[i], hV[i], VxH);
+        for (int r = 0; r < 6; ++r) F0[i][r] = IA[r] + VxH[r];
+        if (f6 && i == 5) {
+          R fw[3], nw[3];
+          for (int r = 0; r < 3; ++r) {
+            fw[r] = Rj[3 * r] * R(f6[0]) + Rj[3 * r + 1] * R(f6[1]) + Rj[3 * r + 2] * R(f6[2]);
+            nw[r] = Rj[3 * r] * R(f6[3]) + Rj[3 * r + 1] * R(f6[4]) + Rj[3 * r + 2] * R(f6[5]);
+          }
+          for (int r = 0; r < 3; ++r) F0[i][r] = F0[i][r] - fw[r];
+          F0[i][3] = F0[i][3] - (nw[0] + (t[1] * fw[2] - t[2] * fw[1]));
+          F0[i][4] = F0[i][4] - (nw[1] + (t[2] * fw[0] - t[0] * fw[2]));
+          F0[i][5] = F0[i][5] - (nw[2] + (t[0] * fw[1] - t[1] * fw[0]));
+        }
+        const R* vl = V[i];
+        const R* w = V[i] + 3;
+        hd[i][0] = m * vl[0] + (w[1] * h[i][2] - w[2] * h[i][1]);
+        hd[i][1] = m * vl[1] + (w[2] * h[i][0] - w[0] * h[i][2]);
+        hd[i][2] = m * vl[2] + (w[0] * h[i][1] - w[1] * h[i][0]);
+        R Ibf[9] = {Ib[i][0], Ib[i][1], Ib[i][2], Ib[i][1], Ib[i][3], Ib[i][4], Ib[i][2], Ib[i][4], Ib[i][5]};
+        R WI[9];
+        for (int q = 0; q < 3; ++q) {
+          WI[q] = w[1] * Ibf[6 + q] - w[2] * Ibf[3 + q];
+          WI[3 + q] = w[2] * Ibf[q] - w[0] * Ibf[6 + q];
+          WI[6 + q] = w[0] * Ibf[3 + q] - w[1] * Ibf[q];
+        }
+        const R vh = vl[0] * h[i][0] + vl[1] * h[i][1] + vl[2] * h[i][2];
+        for (int e = 0; e < 6; ++e) {
+          const int r = iu[e][0], q = iu[e][1];
+          R val = WI[3 * r + q] + WI[3 * q + r] - (h[i][r] * vl[q] + vl[r] * h[i][q]);
+          if (r == q) val = val + R(2.0) * vh;
+          Ibd[i][e] = val;
+        }
+      }
+      // subtree sums (suffix), a_j, e_j, tau0, M
+      R cm[6], ch[6][3], cI[6][6], chd[6][3], cId[6][6], HC[6][6], Fc[6][6];
+      for (int j = 5; j >= 0; --j) {
+        cm[j] = m_[j];
+        for (int r = 0; r < 3; ++r) { ch[j][r] = h[j][r]; chd[j][r] = hd[j][r]; }
+        for (int r = 0; r < 6; ++r) { cI[j][r] = Ib[j][r]; cId[j][r] = Ibd[j][r]; HC[j][r] = hV[j][r]; Fc[j][r] = F0[j][r]; }
+        if (j < 5) {
+          cm[j] = cm[j] + cm[j + 1];
+          for (int r = 0; r < 3; ++r) { ch[j][r] = ch[j][r] + ch[j + 1][r]; chd[j][r] = chd[j][r] + chd[j + 1][r]; }
+          for (int r = 0; r < 6; ++r) {
+            cI[j][r] = cI[j][r] + cI[j + 1][r]; cId[j][r] = cId[j][r] + cId[j + 1][r];
+            HC[j][r] = HC[j][r] + HC[j + 1][r]; Fc[j][r] = Fc[j][r] + Fc[j + 1][r];
+          }
+        }
+      }
+      R aj[6][6], ej[6][6], tau0[6], Lm[6][6];
+      for (int j = 0; j < 6; ++j) {
+        tau0[j] = dot6(S[j], Fc[j]);
+        imul(cm[j], ch[j], cI[j], S[j], aj[j]);
+        R bj[6], cj[6];
+        imul0(chd[j], cId[j], S[j], bj);
+        fcross(S[j], HC[j], cj);
+        for (int r = 0; r < 6; ++r) ej[j][r] = bj[r] - cj[r];
+      }
+      for (int j = 0; j < 6; ++j)
+        for (int kk = 0; kk <= j; ++kk) Lm[j][kk] = Lm[kk][j] = dot6(aj[j], S[kk]);
+      chol6(Lm);
+      R acc[6];
+      for (int r = 0; r < 6; ++r) acc[r] = x[12 + r] - tau0[r];
+      chol6_solve(Lm, acc);
+      // accelerations, full subtree forces
+      R dA[6][6], gI[6][6];
+      for (int j = 0; j < 6; ++j) {
+        for (int r = 0; r < 6; ++r) dA[j][r] = (j ? dA[j - 1][r] : R(0)) + S[j][r] * acc[j];
+        imul(m_[j], h[j], Ib[j], dA[j], gI[j]);
+      }
+      for (int j = 4; j >= 0; --j)
+        for (int r = 0; r < 6; ++r) gI[j][r] = gI[j][r] + gI[j + 1][r];
+      R W[6][6], Z[6][6], y[6][6], z[6][6];
+      for (int j = 0; j < 6; ++j) {
+        R Aj[6], t1[6], t2[6], a1[6], a2[6], a3[6], a4[6], b2[6];
+        for (int r = 0; r < 6; ++r) { Aj[r] = A0[j][r] + dA[j][r]; Fc[j][r] = Fc[j][r] + gI[j][r]; }
+        mcross(S[j], V[j], W[j]);
+        mcross(S[j], Aj, t1);
+        mcross(W[j], V[j], t2);
+        for (int r = 0; r < 6; ++r) Z[j][r] = t1[r] - t2[r];
+        fcross(S[j], Fc[j], a1);
+        imul(cm[j], ch[j], cI[j], Z[j], a2);
+        imul0(chd[j], cId[j], W[j], a3);
+        fcross(W[j], HC[j], a4);
+        for (int r = 0; r < 6; ++r) y[j][r] = a1[r] - a2[r] - a3[r] - a4[r];
+        R b1[6], b3[6];
+        imul0(chd[j], cId[j], S[j], b1);
+        imul(cm[j], ch[j], cI[j], W[j], b2);
+        fcross(S[j], HC[j], b3);
+        for (int r = 0; r < 6; ++r) z[j][r] = b1[r] - R(2.0) * b2[r] + b3[r];
+      }
       R* o = &lin[114 * k];
-      for (int d = 0; d < 12; ++d) {
-        Dual<R> dc[6], ds[6], dv[6], da[6], dtau[6];
-        for (int i = 0; i < 6; ++i) {
-          dc[i] = {c[i], d == i ? R(0) - s[i] : R(0)};
-          ds[i] = {s[i], d == i ? c[i] : R(0)};
-          dv[i] = {x[6 + i], (d - 6 == i) ? R(1) : R(0)};
-          da[i] = {a[i], R(0)};
+      for (int j = 0; j < 6; ++j) {
+        R dq[6], dv[6], em[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
+        for (int r = 0; r < 6; ++r) {
+          if (r >= j) {
+            dq[r] = R(0) - (dot6(aj[r], Z[j]) + dot6(ej[r], W[j]));
+            dv[r] = dot6(ej[r], S[j]) - R(2.0) * dot6(aj[r], W[j]);
+          } else {
+            dq[r] = dot6(S[r], y[j]);
+            dv[r] = dot6(S[r], z[j]);
+          }
         }
-        rnea<R, Dual<R>>(Md, dc, ds, dv, da, true, f6, dtau);
-        R col[6];
-        for (int i = 0; i < 6; ++i) col[i] = R(0) - dtau[i].d;
-        chol6_solve(L, col);
-        for (int i = 0; i < 6; ++i) {
-          if (d < 6) o[6 * i + d] = dt * col[i];
-          else o[36 + 6 * i + d - 6] = (i == d - 6 ? R(1) : R(0)) + dt * col[i];
+        chol6_solve(Lm, dq);
+        chol6_solve(Lm, dv);
+        em[j] = R(1);
+        chol6_solve(Lm, em);
+        for (int r = 0; r < 6; ++r) {
+          o[6 * r + j] = R(0) - dt * dq[r];
+          o[36 + 6 * r + j] = (r == j ? R(1) : R(0)) - dt * dv[r];
+          if (r <= j) o[72 + 6 * r + j] = o[72 + 6 * j + r] = dt * em[r];
         }
       }
-      for (int d = 0; d < 6; ++d) {
-        R e[6] = {R(0), R(0), R(0), R(0), R(0), R(0)};
-        e[d] = R(1);
-        chol6_solve(L, e);
-        for (int i = 0; i <= d; ++i) o[72 + 6 * i + d] = o[72 + 6 * d + i] = dt * e[i];
-      }
-      for (int i = 0; i < 6; ++i) o[108 + i] = a[i];
+      for (int i = 0; i < 6; ++i) o[108 + i] = acc[i];
     }
     for (int k = 0; k < P.N; ++k) {
       const R* q = X + 18 * k;
