@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -17,6 +18,7 @@
 #include "i7m_kernels.h"
 #include "i7m_linearize.h"
 #include "i7m_riccati.h"
+#include "i7m_riccati_mfma.h"
 
 using namespace i7m;
 
@@ -57,6 +59,8 @@ struct i7m_handle {
   ProblemStats* d_stats = nullptr;
   double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
   uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
+  int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
+  int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
   bool has_fext = false;
   size_t goal_cap = 0;
   // timing
@@ -166,8 +170,18 @@ int launch_riccati(i7m_handle* h, const SolveParams& P, const double* xu, const 
                    double* sol) {
   if (P.B == 0) return I7M_OK;
   return timed(h, I7M_K_RICCATI, [&] {
-    hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, h->d_ric_desc, xu, xs, h->d_lin, h->d_cost,
-                       active, h->d_kbuf, sol);
+    if (h->ric_impl == 1)
+      hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, h->d_ric_desc, xu, xs, h->d_lin, h->d_cost,
+                         active, h->d_kbuf, sol);
+    else if (h->ablate == 1)
+      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
+                         active, h->d_kbuf, sol);
+    else if (h->ablate == 2)
+      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
+                         active, h->d_kbuf, sol);
+    else
+      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
+                         active, h->d_kbuf, sol);
   });
 }
 
@@ -274,6 +288,9 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(I7M_EHIP, "hipStreamCreate failed"));
   h->stream = h->own;
+  // developer knob for A/B profiling of the two QP kernels (default: MFMA)
+  if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
+  if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
   // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
   const size_t scratch = std::max(Bm * T, (size_t)256 * 114);

@@ -262,16 +262,22 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
   }
 }
 
-// In-place Cholesky (lower) of a 6x6 SPD matrix; L[i][j] for j<=i.
+// 1/sqrt(d) to full fp64 precision: hardware v_rsq_f64 + one Newton step (instead of the
+// IEEE sqrt and divide sequences, ~25 dependent instructions each).
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  const double y = __builtin_amdgcn_rsq(d);
+  return y * (1.5 - 0.5 * d * y * y);
+}
+
+// In-place Cholesky of a 6x6 SPD matrix: strict lower triangle = L, diagonal = 1 / L_jj.
 __device__ __forceinline__ void chol6(double A[6][6]) {
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     double d = A[j][j];
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
-    d = sqrt(d);
-    A[j][j] = d;
-    const double inv = 1.0 / d;
+    const double inv = rsqrt_nr(d);
+    A[j][j] = inv;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double v = A[i][j];
@@ -281,21 +287,21 @@ __device__ __forceinline__ void chol6(double A[6][6]) {
     }
   }
 }
-// Solve L L^T x = b in place.
+// Solve L L^T x = b in place (L from chol6: diagonal holds the reciprocals).
 __device__ __forceinline__ void chol6_solve(const double L[6][6], double b[6]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     double v = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) v -= L[i][k] * b[k];
-    b[i] = v / L[i][i];
+    b[i] = v * L[i][i];
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     double v = b[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) v -= L[k][i] * b[k];
-    b[i] = v / L[i][i];
+    b[i] = v * L[i][i];
   }
 }
 

@@ -180,39 +180,15 @@ __device__ __forceinline__ void ric_round(double* sh, uint32_t w0, uint32_t w1, 
   sh[oo2] = acc;
 }
 
-// Cholesky (lower) with reciprocal diagonal; solve L L' x = b.
+// Cholesky (lower) with reciprocal diagonal rd; solve L L' x = b.
 __device__ __forceinline__ void chol6r(double A[6][6], double rd[6]) {
+  chol6(A);
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    double d = A[j][j];
-#pragma unroll
-    for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
-    d = sqrt(d);
-    rd[j] = 1.0 / d;
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-      double v = A[i][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) v -= A[i][k] * A[j][k];
-      A[i][j] = v * rd[j];
-    }
-  }
+  for (int j = 0; j < 6; ++j) rd[j] = A[j][j];
 }
 __device__ __forceinline__ void chol6r_solve(const double L[6][6], const double rd[6], double b[6]) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    double v = b[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) v -= L[i][k] * b[k];
-    b[i] = v * rd[i];
-  }
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double v = b[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) v -= L[k][i] * b[k];
-    b[i] = v * rd[i];
-  }
+  (void)rd;
+  chol6_solve(L, b);
 }
 
 __global__ void __launch_bounds__(64) k_riccati(SolveParams P, const uint32_t* __restrict__ desc,

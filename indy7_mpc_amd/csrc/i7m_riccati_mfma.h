@@ -1,0 +1,277 @@
+// i7m_riccati_mfma.h — the SQP subproblem QP solved with fp64 MFMA (v_mfma_f64_16x16x4), one
+// wavefront per problem.  Same math as k_riccati (i7m_riccati.h), reorganised for the matrix
+// cores (reference: the QP handed to OSQP at src/osqp_solver.py:137-143).
+//
+// Homogeneous coordinates x~ = [x; 1] (13 states, padded to a 16x16 tile) fold the affine
+// dynamics offset c and every linear cost term into the matrix products:
+//     A~ = [[A, c], [0, 1]],  B~ = [B; 0],  Q~ = [[Q, q], [q', 0]],  N~ = [0 | r]
+//     W0 = V~ A~,  Qxx = A~' W0 + Q~,  W1 = V~ B~,  H = B~' W1 + R,  G~ = B~' W0 + N~
+//     K~ = -H^-1 G~  (6x13: [K | kff]),   V~ <- Qxx + K~' G~
+// Sixteen 16x16x4 MFMAs per stage.  V~ never leaves the accumulator registers: it is
+// symmetric, so the C/D layout of V~ (lane holds V[(l>>4)+4i][l&15]) is exactly the A-operand
+// layout (V[l&15][4s+(l>>4)]) the next stage needs.  Likewise W0 / W1 / G~ are consumed as
+// B operands straight from their accumulators.  LDS only carries the stage data, H and G~
+// for the 6x6 Cholesky (13 lanes), and K~.
+// MFMA f64 layouts (gfx950; checked by tools/probes/mfma_f64_layout.hip):
+//     A[row=l&15][k=l>>4], B[k=l>>4][col=l&15], D[row=(l>>4)+4i][col=l&15], i=0..3.
+#pragma once
+
+#include "i7m_kernels.h"
+#include "i7m_riccati.h"
+
+namespace i7m {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+enum : int {
+  MO_AQ = 0,     // stage stash: Aq(36) Av(36) Bu(36) a(6) | cost(10) | XU_k(18)  = 142
+  MO_AV = 36,
+  MO_BU = 72,
+  MO_A = 108,
+  MO_W = 114,    // j(6) Qm dQm Rm |e|
+  MO_X = 124,
+  MO_CV = 142,   // 6
+  MO_RU = 148,   // 6   Rm u
+  MO_QV = 154,   // 12  Qm j | dQm v
+  MO_H = 166,    // 36
+  MO_G = 202,    // 78  G~ (6 x 13)
+  MO_KT = 280,   // 78  K~ (6 x 13)
+  MO_ZERO = 358,
+  MO_ONE = 359,
+  MO_TOTAL = 360,
+};
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ABL (diagnostic builds only, results invalid): bit 0 skips the forward rollout, bit 1
+// replaces the Cholesky solve by a copy; used to split the kernel's time.
+template <int ABL>
+__global__ void __launch_bounds__(64) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
+                                                     const double* __restrict__ xs, const double* __restrict__ lin,
+                                                     const double* __restrict__ cost, const int* __restrict__ active,
+                                                     double* __restrict__ kbuf, double* __restrict__ sol) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  const int l = threadIdx.x;
+  const int lr = l & 15, lq = l >> 4;
+  const int N = P.N;
+  const double dt = P.dt;
+  __shared__ double sh[MO_TOTAL];
+  const double* X = xu + (long)b * P.T;
+  const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
+  const double* CB = cost + (long)b * N * COST_STRIDE;
+  double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
+
+  // ---- per-lane operand maps (fixed for the whole kernel)
+  // A~[4s+lq][lr] = sh[offA[s]] + cA[s]
+  int offA[4];
+  double cA[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + lq, c = lr;
+    offA[s] = MO_ZERO;
+    cA[s] = 0.0;
+    if (k < 6) {
+      cA[s] = (c == k) ? 1.0 : (c == k + 6 ? dt : 0.0);
+    } else if (k < 12) {
+      const int i = k - 6;
+      offA[s] = c < 6 ? MO_AQ + 6 * i + c : (c < 12 ? MO_AV + 6 * i + (c - 6) : (c == 12 ? MO_CV + i : MO_ZERO));
+    } else if (k == 12) {
+      cA[s] = (c == 12) ? 1.0 : 0.0;
+    }
+  }
+  // B~[4s+lq][lr] for s = 1, 2
+  int offB[2];
+#pragma unroll
+  for (int s = 1; s < 3; ++s) {
+    const int k = 4 * s + lq;
+    offB[s - 1] = (k >= 6 && lr < 6) ? MO_BU + 6 * (k - 6) + lr : MO_ZERO;
+  }
+  // Q~[lq+4i][lr] = sh[q1[i]] * sh[q2[i]];  R on the u diagonal;  N~ = r in column 12
+  int q1[4], q2[4], oR[4], oN[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = lq + 4 * i, c = lr;
+    q1[i] = MO_ZERO;
+    q2[i] = MO_ZERO;
+    if (r < 6 && c < 6) { q1[i] = MO_QV + r; q2[i] = MO_W + c; }
+    else if (r >= 6 && r < 12 && r == c) { q1[i] = MO_W + 7; q2[i] = MO_ONE; }
+    else if (r < 12 && c == 12) { q1[i] = MO_QV + r; q2[i] = MO_ONE; }
+    else if (r == 12 && c < 12) { q1[i] = MO_QV + c; q2[i] = MO_ONE; }
+    oR[i] = (r == c && r < 6) ? MO_W + 8 : MO_ZERO;
+    oN[i] = (c == 12 && r < 6) ? MO_RU + r : MO_ZERO;
+  }
+  // K~[4s+lq][lr] for s = 0, 1
+  int oK[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int u = 4 * s + lq;
+    oK[s] = (u < 6 && lr < 13) ? MO_KT + 13 * u + lr : MO_ZERO;
+  }
+
+  // ---- terminal cost-to-go V~ = Q~_{N-1}
+  if (l < COST_STRIDE) sh[MO_W + l] = CB[(N - 1) * COST_STRIDE + l];
+  if (l < 12) sh[MO_X + l] = X[18 * (N - 1) + l];
+  if (l == 0) { sh[MO_ZERO] = 0.0; sh[MO_ONE] = 1.0; }
+  __syncthreads();
+  if (l < 12) sh[MO_QV + l] = (l < 6) ? sh[MO_W + 6] * sh[MO_W + l] : sh[MO_W + 7] * sh[MO_X + l];
+  __syncthreads();
+  d4 V;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) V[i] = sh[q1[i]] * sh[q2[i]];
+
+  auto src = [&](int k, int e) -> const double* {
+    if (e < LIN_STRIDE) return LINb + (long)k * LIN_STRIDE + e;
+    if (e < LIN_STRIDE + COST_STRIDE) return CB + k * COST_STRIDE + (e - LIN_STRIDE);
+    return X + 18 * k + (e - LIN_STRIDE - COST_STRIDE);
+  };
+  const int e2 = (l + 128 < 142) ? l + 128 : 141;
+  double p0 = *src(N - 2, l), p1 = *src(N - 2, l + 64), p2 = *src(N - 2, e2);
+
+  for (int k = N - 2; k >= 0; --k) {
+    __syncthreads();
+    sh[MO_AQ + l] = p0;
+    sh[MO_AQ + l + 64] = p1;
+    if (l + 128 < 142) sh[MO_AQ + l + 128] = p2;
+    __syncthreads();
+    if (k > 0) { p0 = *src(k - 1, l); p1 = *src(k - 1, l + 64); p2 = *src(k - 1, e2); }
+    if (l < 6) {  // c_v = v + dt a - (Aq q + Av v + Bu u)   (src/osqp_solver.py:76-81)
+      double acc = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj)
+        acc += sh[MO_AQ + 6 * l + jj] * sh[MO_X + jj] + sh[MO_AV + 6 * l + jj] * sh[MO_X + 6 + jj] +
+               sh[MO_BU + 6 * l + jj] * sh[MO_X + 12 + jj];
+      sh[MO_CV + l] = (sh[MO_X + 6 + l] + sh[MO_A + l] * dt) - acc;
+    } else if (l < 12) {
+      sh[MO_RU + l - 6] = sh[MO_W + 8] * sh[MO_X + 12 + (l - 6)];
+    } else if (l < 24) {
+      const int r = l - 12;
+      sh[MO_QV + r] = (r < 6) ? sh[MO_W + 6] * sh[MO_W + r] : sh[MO_W + 7] * sh[MO_X + r];
+    }
+    __syncthreads();
+    double bA[4], bB[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
+    bB[0] = sh[offB[0]];
+    bB[1] = sh[offB[1]];
+    d4 Qi, Ri, Ni;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Qi[i] = sh[q1[i]] * sh[q2[i]];
+      Ri[i] = sh[oR[i]];
+      Ni[i] = sh[oN[i]];
+    }
+    // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
+    // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
+    d4 W0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
+    d4 Z00 = Qi;
+    if (lq == 0) Z00[3] += W0[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+    // W1 = V B~ ; H = B~' W1 + R ; G~ = B~' W0 + N~   (B~ rows 6..11 only: k-steps 1, 2)
+    d4 W1 = {0.0, 0.0, 0.0, 0.0};
+    W1 = mfma(V[1], bB[0], W1);
+    W1 = mfma(V[2], bB[1], W1);
+    d4 Z11 = mfma(bB[0], W1[1], Ri);
+    Z11 = mfma(bB[1], W1[2], Z11);
+    d4 Z10 = mfma(bB[0], W0[1], Ni);
+    Z10 = mfma(bB[1], W0[2], Z10);
+    // H (6x6) and G~ (6x13) to LDS: rows lq + 4i < 6
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = lq + 4 * i;
+      if (r < 6) {
+        if (lr < 6) sh[MO_H + 6 * r + lr] = Z11[i];
+        if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
+      }
+    }
+    __syncthreads();
+    if ((ABL & 2) && l < 13) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + l] = -sh[MO_G + 13 * i + l] * 1e-3;
+    } else if (l < 13) {
+      double L[6][6], rd[6], rhs[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 6; ++jj) L[i][jj] = sh[MO_H + 6 * i + jj];
+      chol6r(L, rd);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) rhs[i] = sh[MO_G + 13 * i + l];
+      chol6r_solve(L, rd, rhs);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + l] = -rhs[i];
+    }
+    __syncthreads();
+    // V~ <- Qxx + K~' G~
+    V = mfma(sh[oK[0]], Z10[0], Z00);
+    V = mfma(sh[oK[1]], Z10[1], V);
+    // K~ (78) and c_v (6) -> global for the forward rollout (each element loaded back by the
+    // same lane that stores it)
+    double* kk = KB + (long)k * KBUF_STRIDE;
+    kk[l] = sh[MO_KT + l];
+    if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
+  }
+
+  // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c
+  if (ABL & 1) return;
+  double* S = sol + (long)b * P.T;
+  double* sx = sh + MO_H;        // x double buffer [2][12]
+  double* su = sh + MO_H + 24;   // u (6)
+  double* sk = sh + MO_KT;       // K~ (6 x 13)
+  double* sc = sh + MO_CV;       // c_v (6)
+  double* sl = sh + MO_AQ;       // Aq Av Bu (108)
+  auto fsrc = [&](int k, int e) -> const double* {
+    return (e < KBUF_STRIDE) ? KB + (long)k * KBUF_STRIDE + e : LINb + (long)k * LIN_STRIDE + (e - KBUF_STRIDE);
+  };
+  auto fdst = [&](int e) -> double* { return (e < 78) ? sk + e : (e < 84 ? sc + (e - 78) : sl + (e - 84)); };
+  __syncthreads();
+  double f0 = *fsrc(0, l), f1 = *fsrc(0, l + 64), f2 = *fsrc(0, l + 128);
+  if (l < 12) {
+    const double x0 = xs[(long)b * 12 + l];
+    sx[l] = x0;
+    S[l] = x0;
+  }
+  for (int k = 0; k < N - 1; ++k) {
+    const int cur = k & 1;
+    __syncthreads();
+    *fdst(l) = f0;
+    *fdst(l + 64) = f1;
+    *fdst(l + 128) = f2;
+    __syncthreads();
+    if (k + 1 < N - 1) { f0 = *fsrc(k + 1, l); f1 = *fsrc(k + 1, l + 64); f2 = *fsrc(k + 1, l + 128); }
+    const double* x = sx + 12 * cur;
+    if (l < 6) {
+      double acc = sk[13 * l + 12];
+#pragma unroll
+      for (int jj = 0; jj < 12; ++jj) acc += sk[13 * l + jj] * x[jj];
+      su[l] = acc;
+      S[18 * k + 12 + l] = acc;
+    }
+    __syncthreads();
+    if (l < 12) {
+      double nx;
+      if (l < 6) {
+        nx = x[l] + dt * x[6 + l];
+      } else {
+        const int i = l - 6;
+        double acc = sc[i];
+#pragma unroll
+        for (int jj = 0; jj < 6; ++jj)
+          acc += sl[6 * i + jj] * x[jj] + sl[36 + 6 * i + jj] * x[6 + jj] + sl[72 + 6 * i + jj] * su[jj];
+        nx = acc;
+      }
+      sx[12 * (cur ^ 1) + l] = nx;
+      S[18 * (k + 1) + l] = nx;
+    }
+  }
+}
+
+}  // namespace i7m
