@@ -61,6 +61,7 @@ struct i7m_handle {
   uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
   int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
   int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
+  bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
   size_t goal_cap = 0;
   // timing
@@ -161,8 +162,12 @@ int launch_linearize(i7m_handle* h, const SolveParams& P, const double* xu, cons
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
   return timed(h, I7M_K_LIN, [&] {
-    hipLaunchKernelGGL(k_linearize, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
-                       h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
+    if (h->spec)
+      hipLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
+                         h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
+    else
+      hipLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
+                         h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
   });
 }
 
@@ -189,8 +194,15 @@ int launch_linesearch(i7m_handle* h, const SolveParams& P, double* xu, const dou
                       int* active, ProblemStats* st, double* alpha_out, int iter, int mode) {
   if (P.B == 0) return I7M_OK;
   return timed(h, I7M_K_LINESEARCH, [&] {
-    hipLaunchKernelGGL(k_linesearch, dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
-                       h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+    if (h->ablate == 4)
+      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
+                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+    else if (h->spec)
+      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
+                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+    else
+      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
+                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
   });
 }
 
@@ -309,6 +321,9 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (hipMemcpy(h->d_ric_desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(I7M_EHIP, "descriptor upload failed"));
   DevModel dm = make_dev_model(cfg->model);
+  // the Indy7-specialised kernels are used only for a model bit-identical to the baked one
+  h->spec = std::memcmp(&dm, &kIndy7Model, sizeof(DevModel)) == 0;
+  if (const char* e = std::getenv("I7M_GENERIC")) h->spec = h->spec && std::atoi(e) == 0;
   if (hipMemcpy(h->d_model, &dm, sizeof(dm), hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(I7M_EHIP, "model upload failed"));
   *out = h;

@@ -100,6 +100,7 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
   T f[6][6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
     const double* R = M.Rp[i];
     const double* t = M.tp[i];
     // parent -> child: y = Rz^T Rp^T (x - t x w)
@@ -148,6 +149,7 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
+    __builtin_amdgcn_sched_barrier(0);
     tau[i] = f[i][5];
     if (i > 0) {
       const double* R = M.Rp[i];
@@ -174,23 +176,18 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
   }
 }
 
-// Composite-rigid-body algorithm: joint-space inertia M (lower triangle filled, symmetric).
+// Composite-rigid-body algorithm: joint-space inertia M (full, symmetric).  One running
+// composite inertia (m, h, I about the current joint origin) is carried from the tip to the
+// base, so only ~10 doubles of composite state are live at any time.
 __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], const double s[6], double Mq[6][6]) {
-  // composite inertia of body i in frame i: (m, h[3], I[6] about origin)
-  double cm[6], ch[6][3], cI[6][6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    cm[i] = Md.m[i];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ch[i][k] = Md.h[i][k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) cI[i][k] = Md.Io[i][k];
-  }
+  double cm = Md.m[5], ch[3] = {Md.h[5][0], Md.h[5][1], Md.h[5][2]};
+  double cI[6] = {Md.Io[5][0], Md.Io[5][1], Md.Io[5][2], Md.Io[5][3], Md.Io[5][4], Md.Io[5][5]};
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
+    __builtin_amdgcn_sched_barrier(0);
     // column i: F = IC_i S, S = (0; e_z): lin = e_z x h = (-h_y, h_x, 0), ang = I e_z
-    double fl[3] = {-ch[i][1], ch[i][0], 0.0};
-    double fn[3] = {cI[i][2], cI[i][4], cI[i][5]};
+    double fl[3] = {-ch[1], ch[0], 0.0};
+    double fn[3] = {cI[2], cI[4], cI[5]};
     Mq[i][i] = fn[2];
 #pragma unroll
     for (int j = i; j >= 1; --j) {
@@ -214,15 +211,14 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
       Mq[j - 1][i] = fn[2];
     }
     if (i > 0) {
-      // IC_{i-1} += X_i^* IC_i X_i^{-1}: rotate (R = Rp Rz), then shift by t
+      // IC_{i-1} = I_{i-1} + X_i^* IC_i X_i^{-1}: rotate (R = Rp Rz), then shift by t
       const double* R = Md.Rp[i];
       const double* t = Md.tp[i];
-      const double m = cm[i];
-      double hz[3] = {c[i] * ch[i][0] - s[i] * ch[i][1], s[i] * ch[i][0] + c[i] * ch[i][1], ch[i][2]};
+      const double m = cm;
+      double hz[3] = {c[i] * ch[0] - s[i] * ch[1], s[i] * ch[0] + c[i] * ch[1], ch[2]};
       double hr[3];
       rp(R, hz, hr);
-      // Rz I Rz^T
-      const double* I = cI[i];
+      const double* I = cI;
       const double cc = c[i] * c[i], ss = s[i] * s[i], cs = c[i] * s[i];
       double A[3][3];
       A[0][0] = cc * I[0] - 2.0 * cs * I[1] + ss * I[3];
@@ -232,7 +228,6 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
       A[1][2] = s[i] * I[2] + c[i] * I[4];
       A[2][2] = I[5];
       A[1][0] = A[0][1]; A[2][0] = A[0][2]; A[2][1] = A[1][2];
-      // B = Rp A Rp^T
       double RA[3][3];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
@@ -247,17 +242,20 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
       const double tt = t[0] * t[0] + t[1] * t[1] + t[2] * t[2];
       const double dg = 2.0 * ht + m * tt;
       const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+      double nI[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int r = iu[k][0], q = iu[k][1];
         double v = Bm[r][q] - (t[r] * hr[q] + hr[r] * t[q]) - m * t[r] * t[q];
         if (r == q) v += dg;
-        cI[i - 1][k] += v;
+        nI[k] = Md.Io[i - 1][k] + v;
       }
-      ch[i - 1][0] += hr[0] + m * t[0];
-      ch[i - 1][1] += hr[1] + m * t[1];
-      ch[i - 1][2] += hr[2] + m * t[2];
-      cm[i - 1] += m;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cI[k] = nI[k];
+      ch[0] = Md.h[i - 1][0] + (hr[0] + m * t[0]);
+      ch[1] = Md.h[i - 1][1] + (hr[1] + m * t[1]);
+      ch[2] = Md.h[i - 1][2] + (hr[2] + m * t[2]);
+      cm = Md.m[i - 1] + m;
     }
   }
 }
@@ -309,12 +307,13 @@ __device__ __forceinline__ void chol6_solve(const double L[6][6], double b[6]) {
 __device__ __forceinline__ void forward_dynamics(const DevModel& Md, const double c[6], const double s[6],
                                                  const double v[6], const double tau[6], const double* fext6,
                                                  double L[6][6], double a[6]) {
-  crba(Md, c, s, L);
-  chol6(L);
   double z[6] = {0, 0, 0, 0, 0, 0}, b[6];
   rnea<double>(Md, c, s, v, z, true, fext6, b);
 #pragma unroll
   for (int i = 0; i < 6; ++i) a[i] = tau[i] - b[i];
+  __builtin_amdgcn_sched_barrier(0);
+  crba(Md, c, s, L);
+  chol6(L);
   chol6_solve(L, a);
 }
 
@@ -347,6 +346,7 @@ __device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], co
   double zs[6][3], ps[6][3];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
     const double* Rp = Md.Rp[i];
     const double* t = Md.tp[i];
     double np[3];

@@ -13,6 +13,7 @@
 #pragma once
 
 #include "i7m_dynamics.h"
+#include "i7m_indy7_model.h"
 
 namespace i7m {
 
@@ -96,6 +97,8 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // itself, src/osqp_sqp.py:52-55), 1..8 = alphas 1, 1/2, ..., 1/128.  R = max(1, 64/N)
 // candidates per round; the first accepted candidate in alpha order wins (identical to the
 // sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha.
+// SPEC: Indy7 constants baked in (kIndy7Model, generated from the URDF) instead of read from Mg.
+template <bool SPEC, int ABL = 0>
 __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    double* __restrict__ xu, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
@@ -110,7 +113,7 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   const int R = (N >= 64) ? 1 : 64 / N;
   const int slot = l / N;
   const int k = l - slot * N;
-  const DevModel& Md = *Mg;
+  const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   double* X = xu + (long)b * P.T;
   const double* S = sol + (long)b * P.T;
   __shared__ double part[64][4];
@@ -121,24 +124,37 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   for (int c0 = 0; c0 < 1 + NALPHA && found < 0; c0 += R) {
     const int cand = c0 + slot;
     if (slot < R && k < N && cand < 1 + NALPHA) {
+      // knot k (18 values; the last knot has no u) and the state of knot k+1 (12 values),
+      // fully unrolled so they stay in registers
+      const bool last = (k == N - 1);
+      const double al = (cand == 0) ? 0.0 : alphas[cand - 1];
+      const double* Xk = X + 18 * k;
+      const double* Sk = S + 18 * k;
+      const double* Xn = X + 18 * (last ? k : k + 1);
+      const double* Sn = S + 18 * (last ? k : k + 1);
       double x[18], xn[12];
-      const int nk = (k < N - 1) ? 18 : 12;
-      if (cand == 0) {
-        for (int i = 0; i < nk; ++i) x[i] = X[18 * k + i];
-        if (k < N - 1)
-          for (int i = 0; i < 12; ++i) xn[i] = X[18 * (k + 1) + i];
-      } else {
-        const double al = alphas[cand - 1];
-        for (int i = 0; i < nk; ++i) x[i] = X[18 * k + i] + al * (S[18 * k + i] - X[18 * k + i]);
-        if (k < N - 1)
-          for (int i = 0; i < 12; ++i) xn[i] = X[18 * (k + 1) + i] + al * (S[18 * (k + 1) + i] - X[18 * (k + 1) + i]);
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        const int ii = (last && i >= 12) ? 0 : i;
+        const double xv = Xk[ii];
+        x[i] = (cand == 0) ? xv : xv + al * (Sk[ii] - xv);
+      }
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        const double xv = Xn[i];
+        xn[i] = (cand == 0) ? xv : xv + al * (Sn[i] - xv);
       }
       double o[4];
-      merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride,
-                 fext ? fext + 6L * b : nullptr, o);
+      if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
+        o[0] = x[0] * x[1]; o[1] = x[6] * x[6]; o[2] = x[12] * xn[0]; o[3] = xn[6] + x[17];
+      } else {
+        merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride,
+                   fext ? fext + 6L * b : nullptr, o);
+      }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
         double dd = 0.0;
+#pragma unroll
         for (int i = 0; i < 12; ++i) {
           const double t = x[i] - X[i];
           dd += t * t;

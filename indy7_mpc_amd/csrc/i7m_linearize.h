@@ -61,11 +61,12 @@ __device__ __forceinline__ void imul(double m, const double* h, const double* I,
   o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
 }
 
+template <bool SPEC>
 __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
                                                   const double* __restrict__ xu, const double* __restrict__ goals,
                                                   const double* __restrict__ fext, const int* __restrict__ active,
                                                   double* __restrict__ lin, double* __restrict__ cost) {
-  const DevModel& Md = *Mg;
+  const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   const int l = threadIdx.x;
   const int g = l / 6;
   const int j = l - 6 * g;

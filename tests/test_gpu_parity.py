@@ -124,3 +124,17 @@ def test_analytic_linearisation_equals_dual_number_path(lib, model):
         np.testing.assert_allclose(L[n, 36:72].reshape(6, 6), np.eye(6) + dt * dv[n], rtol=1e-9, atol=1e-11)
         np.testing.assert_allclose(L[n, 72:108].reshape(6, 6), dt * Mi[n], rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(L[n, 108:], a[n], rtol=1e-9, atol=1e-9)
+
+
+def test_specialised_and_generic_model_kernels_agree(lib, model, monkeypatch):
+    """The Indy7-baked kernels (kIndy7Model) and the runtime-model kernels give the same SQP."""
+    N, B = 16, 8
+    xcur, goals, XU = synthetic_batch(B, N, seed=23)
+    spec = _handle(lib, model, N, B)
+    monkeypatch.setenv("I7M_GENERIC", "1")
+    gen = _handle(lib, model, N, B)
+    o1, s1 = spec.solve(xcur, goals, XU)
+    o2, s2 = gen.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(s1["qp_iters"], s2["qp_iters"])
+    np.testing.assert_array_equal(s1["alphas"], s2["alphas"])
+    assert np.abs(o1 - o2).max() <= 1e-10 * np.abs(o2).max()
