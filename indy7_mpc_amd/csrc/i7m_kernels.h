@@ -116,63 +116,76 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   double* X = xu + (long)b * P.T;
   const double* S = sol + (long)b * P.T;
+  // the problem's XU and QP minimiser, staged once in LDS for every round
+  __shared__ double sX[18 * MAXN], sS[18 * MAXN];
   __shared__ double part[64][4];
   __shared__ double merit[9];
+  for (int e = l; e < P.T; e += 64) {
+    sX[e] = X[e];
+    sS[e] = S[e];
+  }
   const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
+  const bool pow2 = (N & (N - 1)) == 0;
+  const double* goal = goals + (long)b * N * P.goal_stride + (long)(k < N ? k : 0) * P.goal_stride;
+  const double* f6 = fext ? fext + 6L * b : nullptr;
+  __syncthreads();
   double base = 0.0;
   int found = -1;
   for (int c0 = 0; c0 < 1 + NALPHA && found < 0; c0 += R) {
     const int cand = c0 + slot;
+    double o[4] = {0.0, 0.0, 0.0, 0.0};
     if (slot < R && k < N && cand < 1 + NALPHA) {
-      // knot k (18 values; the last knot has no u) and the state of knot k+1 (12 values),
-      // fully unrolled so they stay in registers
+      // knot k (18 values; the last knot has no u) and the state of knot k+1 (12 values)
       const bool last = (k == N - 1);
       const double al = (cand == 0) ? 0.0 : alphas[cand - 1];
-      const double* Xk = X + 18 * k;
-      const double* Sk = S + 18 * k;
-      const double* Xn = X + 18 * (last ? k : k + 1);
-      const double* Sn = S + 18 * (last ? k : k + 1);
+      const int ok = 18 * k, on = 18 * (last ? k : k + 1);
       double x[18], xn[12];
 #pragma unroll
       for (int i = 0; i < 18; ++i) {
         const int ii = (last && i >= 12) ? 0 : i;
-        const double xv = Xk[ii];
-        x[i] = (cand == 0) ? xv : xv + al * (Sk[ii] - xv);
+        const double xv = sX[ok + ii];
+        x[i] = (cand == 0) ? xv : xv + al * (sS[ok + ii] - xv);
       }
 #pragma unroll
       for (int i = 0; i < 12; ++i) {
-        const double xv = Xn[i];
-        xn[i] = (cand == 0) ? xv : xv + al * (Sn[i] - xv);
+        const double xv = sX[on + i];
+        xn[i] = (cand == 0) ? xv : xv + al * (sS[on + i] - xv);
       }
-      double o[4];
       if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
         o[0] = x[0] * x[1]; o[1] = x[6] * x[6]; o[2] = x[12] * xn[0]; o[3] = xn[6] + x[17];
       } else {
-        merit_knot(Md, P, k, x, xn, goals + (long)b * N * P.goal_stride + (long)k * P.goal_stride,
-                   fext ? fext + 6L * b : nullptr, o);
+        merit_knot(Md, P, k, x, xn, goal, f6, o);
       }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
         double dd = 0.0;
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-          const double t = x[i] - X[i];
+          const double t = x[i] - sX[i];
           dd += t * t;
         }
         o[3] += sqrt(dd);
       }
-      part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
     }
-    __syncthreads();
-    if (l < R && c0 + l < 1 + NALPHA) {
-      double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
-      for (int kk = 0; kk < N; ++kk) {
-        qc += part[l * N + kk][0];
-        vc += part[l * N + kk][1];
-        uc += part[l * N + kk][2];
-        cv += part[l * N + kk][3];
+    if (pow2) {
+      // tree-sum the N knots of each candidate slot with shuffles (segments of width N)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        for (int off = N >> 1; off >= 1; off >>= 1) o[j] += __shfl_xor(o[j], off, 64);
+      if (k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
+    } else {
+      part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
+      __syncthreads();
+      if (l < R && c0 + l < 1 + NALPHA) {
+        double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
+        for (int kk = 0; kk < N; ++kk) {
+          qc += part[l * N + kk][0];
+          vc += part[l * N + kk][1];
+          uc += part[l * N + kk][2];
+          cv += part[l * N + kk][3];
+        }
+        merit[c0 + l] = qc + vc + uc + P.mu * cv;
       }
-      merit[c0 + l] = qc + vc + uc + P.mu * cv;
     }
     __syncthreads();
     base = merit[0];
@@ -199,8 +212,9 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   }
   double ss = 0.0;
   for (int e = l; e < P.T; e += 64) {
-    const double stp = alpha * (S[e] - X[e]);
-    X[e] = X[e] + stp;
+    const double xv = sX[e];
+    const double stp = alpha * (sS[e] - xv);
+    X[e] = xv + stp;
     ss += stp * stp;
   }
   // wave reduction
