@@ -45,10 +45,27 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// v from lane `src` (wave-uniform src) into every lane, via two v_readlane_b32 (SGPR broadcast).
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// 1/d to full fp64 precision: v_rcp_f64 + two Newton steps.
+__device__ __forceinline__ double rcp_nr(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  y = y * (2.0 - d * y);
+  return y * (2.0 - d * y);
+}
+
 // ABL (diagnostic builds only, results invalid): bit 0 skips the forward rollout, bit 1
-// replaces the Cholesky solve by a copy; used to split the kernel's time.
+// replaces the Gauss-Jordan solve by a scaling; used to split the kernel's time.
+// 4 waves/SIMD (<= 128 VGPRs, MFMA accumulators in VGPRs): B = 4096 single-wave problems fit the
+// 1024 SIMDs in one round.
 template <int ABL>
-__global__ void __launch_bounds__(64) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
                                                      const double* __restrict__ xs, const double* __restrict__ lin,
                                                      const double* __restrict__ cost, const int* __restrict__ active,
                                                      double* __restrict__ kbuf, double* __restrict__ sol) {
@@ -193,21 +210,33 @@ __global__ void __launch_bounds__(64) k_riccati_mfma(SolveParams P, const double
       }
     }
     __syncthreads();
-    if ((ABL & 2) && l < 13) {
+    // K~ = -H^-1 G~ by Gauss-Jordan on [H | G~] (6 x 19), one column per lane (lanes 0..18):
+    // the pivot column lives in lane p and is broadcast with v_readlane, so the factorisation is
+    // done once (not once per right-hand side) and needs no LDS round trip.  SPD H: no pivoting.
+    {
+      double E[6];
+      const int cc = l < 19 ? l : 18;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + l] = -sh[MO_G + 13 * i + l] * 1e-3;
-    } else if (l < 13) {
-      double L[6][6], rd[6], rhs[6];
+      for (int i = 0; i < 6; ++i) E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : sh[MO_G + 13 * i + (cc - 6)];
+      if (ABL & 2) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < 6; ++i) E[i] *= 1e-3;
+      } else {
 #pragma unroll
-        for (int jj = 0; jj < 6; ++jj) L[i][jj] = sh[MO_H + 6 * i + jj];
-      chol6r(L, rd);
+        for (int p = 0; p < 6; ++p) {
+          double Pc[6];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) rhs[i] = sh[MO_G + 13 * i + l];
-      chol6r_solve(L, rd, rhs);
+          for (int i = 0; i < 6; ++i) Pc[i] = readlane_f64(E[i], p);
+          const double inv = rcp_nr(Pc[p]);
+          const double ep = E[p] * inv;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + l] = -rhs[i];
+          for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
+        }
+      }
+      if (l >= 6 && l < 19) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (l - 6)] = -E[i];
+      }
     }
     __syncthreads();
     // V~ <- Qxx + K~' G~
@@ -220,57 +249,91 @@ __global__ void __launch_bounds__(64) k_riccati_mfma(SolveParams P, const double
     if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
   }
 
-  // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c
+  // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
+  // Lane l < 12 holds x_l and lane m < 6 holds u_m; every lane sees the full vectors through
+  // v_readlane.  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
+  // (3 per lane) FD stages ahead into registers, dropped into one LDS slot, and each lane reads
+  // its own rows from there (lanes 0..5: a K~ row; lanes 6..11: c_v + Aq/Av/Bu rows).  Stage 0
+  // is still in LDS from the last backward step.
   if (ABL & 1) return;
+  constexpr int FD = 2;
+  __syncthreads();  // kbuf stores of the backward sweep -> loads below (same workgroup)
   double* S = sol + (long)b * P.T;
-  double* sx = sh + MO_H;        // x double buffer [2][12]
-  double* su = sh + MO_H + 24;   // u (6)
-  double* sk = sh + MO_KT;       // K~ (6 x 13)
-  double* sc = sh + MO_CV;       // c_v (6)
-  double* sl = sh + MO_AQ;       // Aq Av Bu (108)
+  const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
+  const int ik = l < 6 ? l : 0;
   auto fsrc = [&](int k, int e) -> const double* {
     return (e < KBUF_STRIDE) ? KB + (long)k * KBUF_STRIDE + e : LINb + (long)k * LIN_STRIDE + (e - KBUF_STRIDE);
   };
-  auto fdst = [&](int e) -> double* { return (e < 78) ? sk + e : (e < 84 ? sc + (e - 78) : sl + (e - 84)); };
-  __syncthreads();
-  double f0 = *fsrc(0, l), f1 = *fsrc(0, l + 64), f2 = *fsrc(0, l + 128);
-  if (l < 12) {
-    const double x0 = xs[(long)b * 12 + l];
-    sx[l] = x0;
-    S[l] = x0;
+  double f[FD][3];
+#pragma unroll
+  for (int d = 0; d < FD; ++d) {
+    const int kk = (1 + d < N - 1) ? 1 + d : 0;
+    f[d][0] = *fsrc(kk, l);
+    f[d][1] = *fsrc(kk, l + 64);
+    f[d][2] = *fsrc(kk, l + 128);
   }
+  double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
+  if (l < 12) S[l] = xreg;
+  int okt = MO_KT, ocv = MO_CV, oli = MO_AQ;  // stage-0 locations (backward stash)
   for (int k = 0; k < N - 1; ++k) {
-    const int cur = k & 1;
-    __syncthreads();
-    *fdst(l) = f0;
-    *fdst(l + 64) = f1;
-    *fdst(l + 128) = f2;
-    __syncthreads();
-    if (k + 1 < N - 1) { f0 = *fsrc(k + 1, l); f1 = *fsrc(k + 1, l + 64); f2 = *fsrc(k + 1, l + 128); }
-    const double* x = sx + 12 * cur;
-    if (l < 6) {
-      double acc = sk[13 * l + 12];
+    if (k > 0) {
+      __syncthreads();
+      sh[l] = f[0][0];
+      sh[l + 64] = f[0][1];
+      sh[l + 128] = f[0][2];
 #pragma unroll
-      for (int jj = 0; jj < 12; ++jj) acc += sk[13 * l + jj] * x[jj];
-      su[l] = acc;
-      S[18 * k + 12 + l] = acc;
-    }
-    __syncthreads();
-    if (l < 12) {
-      double nx;
-      if (l < 6) {
-        nx = x[l] + dt * x[6 + l];
-      } else {
-        const int i = l - 6;
-        double acc = sc[i];
-#pragma unroll
-        for (int jj = 0; jj < 6; ++jj)
-          acc += sl[6 * i + jj] * x[jj] + sl[36 + 6 * i + jj] * x[6 + jj] + sl[72 + 6 * i + jj] * su[jj];
-        nx = acc;
+      for (int d = 0; d + 1 < FD; ++d) {
+        f[d][0] = f[d + 1][0];
+        f[d][1] = f[d + 1][1];
+        f[d][2] = f[d + 1][2];
       }
-      sx[12 * (cur ^ 1) + l] = nx;
-      S[18 * (k + 1) + l] = nx;
+      const int kn = (k + FD < N - 1) ? k + FD : k;
+      f[FD - 1][0] = *fsrc(kn, l);
+      f[FD - 1][1] = *fsrc(kn, l + 64);
+      f[FD - 1][2] = *fsrc(kn, l + 128);
+      okt = 0;
+      ocv = 78;
+      oli = 84;
+      __syncthreads();
     }
+    double r[19];
+    if (l < 6) {
+#pragma unroll
+      for (int j = 0; j < 13; ++j) r[j] = sh[okt + 13 * ik + j];
+#pragma unroll
+      for (int j = 13; j < 19; ++j) r[j] = 0.0;
+    } else {
+      r[0] = sh[ocv + iv];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        r[1 + j] = sh[oli + 6 * iv + j];
+        r[7 + j] = sh[oli + 36 + 6 * iv + j];
+        r[13 + j] = sh[oli + 72 + 6 * iv + j];
+      }
+    }
+    double X[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
+    // u (lanes 0..5): two partial sums to halve the dependency chain
+    double ua = r[12], ub = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
+    const double ureg = ua + ub;
+    if (l < 6) S[18 * k + 12 + l] = ureg;
+    double U[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
+    double va = r[0], vb = 0.0, vc = 0.0, vq = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      va += r[1 + j] * X[j];
+      vb += r[7 + j] * X[6 + j];
+      vc += r[13 + j] * U[j];
+      vq = (l == j) ? X[6 + j] : vq;
+    }
+    const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
+    xreg = nx;
+    if (l < 12) S[18 * (k + 1) + l] = nx;
   }
 }
 
