@@ -40,6 +40,8 @@ int fail(int code, const std::string& msg) {
       return fail(I7M_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                  \
   } while (0)
 
+constexpr int I7M_MAX_CHUNKS = 4;
+
 struct Timing {
   int kid;
   hipEvent_t a, b;
@@ -64,6 +66,10 @@ struct i7m_handle {
   bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
   size_t goal_cap = 0;
+  // concurrent problem ranges (run_sqp): worker streams + fork/join events
+  int chunks = 0;  // 0: automatic (chunks_for), else I7M_CHUNKS
+  hipStream_t workers[I7M_MAX_CHUNKS] = {};
+  hipEvent_t fork = nullptr, join[I7M_MAX_CHUNKS] = {};
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -141,83 +147,136 @@ hipEvent_t get_event(i7m_handle* h) {
 }
 
 template <class F>
-int timed(i7m_handle* h, int kid, F&& launch) {
+int timed(i7m_handle* h, hipStream_t s, int kid, F&& launch) {
   hipEvent_t a = nullptr, b = nullptr;
   if (h->timing) {
     a = get_event(h);
     b = get_event(h);
-    if (a && b) HIPCHK(hipEventRecord(a, h->stream));
+    if (a && b) HIPCHK(hipEventRecord(a, s));
   }
   launch();
   HIPCHK(hipGetLastError());
   if (h->timing && a && b) {
-    HIPCHK(hipEventRecord(b, h->stream));
+    HIPCHK(hipEventRecord(b, s));
     h->ev.push_back({kid, a, b});
   }
   return I7M_OK;
 }
 
-int launch_linearize(i7m_handle* h, const SolveParams& P, const double* xu, const double* goals, const int* active) {
+// Per-problem work buffers of a contiguous range of problems [b0, b0 + B): every kernel indexes
+// them by its local problem index, so a range is just offset base pointers.
+struct Bufs {
+  double* lin;
+  double* cost;
+  double* kbuf;
+  const double* fext;  // nullptr: no external wrench
+};
+
+Bufs bufs_at(const i7m_handle* h, long b0) {
+  const long N = h->cfg.N;
+  return {h->d_lin + b0 * (N - 1) * LIN_STRIDE, h->d_cost + b0 * N * COST_STRIDE,
+          h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr};
+}
+
+int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
+                     const double* goals, const int* active) {
   const long knots = (long)P.B * P.N;
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
-  return timed(h, I7M_K_LIN, [&] {
+  return timed(h, s, I7M_K_LIN, [&] {
     if (h->spec)
-      hipLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
-                         h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
+      hipLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
+                         W.lin, W.cost);
     else
-      hipLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, h->stream, h->d_model, P, xu, goals,
-                         h->has_fext ? h->d_fext : nullptr, active, h->d_lin, h->d_cost);
+      hipLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
+                         W.lin, W.cost);
   });
 }
 
-int launch_riccati(i7m_handle* h, const SolveParams& P, const double* xu, const double* xs, const int* active,
-                   double* sol) {
+int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
+                   const double* xs, const int* active, double* sol) {
   if (P.B == 0) return I7M_OK;
-  return timed(h, I7M_K_RICCATI, [&] {
+  return timed(h, s, I7M_K_RICCATI, [&] {
     if (h->ric_impl == 1)
-      hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, h->stream, P, h->d_ric_desc, xu, xs, h->d_lin, h->d_cost,
-                         active, h->d_kbuf, sol);
+      hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
+                         W.kbuf, sol);
     else if (h->ablate == 1)
-      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
-                         active, h->d_kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
     else if (h->ablate == 2)
-      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
-                         active, h->d_kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
     else
-      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, h->stream, P, xu, xs, h->d_lin, h->d_cost,
-                         active, h->d_kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
   });
 }
 
-int launch_linesearch(i7m_handle* h, const SolveParams& P, double* xu, const double* sol, const double* goals,
-                      int* active, ProblemStats* st, double* alpha_out, int iter, int mode) {
+int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, double* xu,
+                      const double* sol, const double* goals, int* active, ProblemStats* st, double* alpha_out,
+                      int iter, int mode) {
   if (P.B == 0) return I7M_OK;
-  return timed(h, I7M_K_LINESEARCH, [&] {
+  return timed(h, s, I7M_K_LINESEARCH, [&] {
     if (h->ablate == 4)
-      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
-                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode);
     else if (h->spec)
-      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
-                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode);
     else
-      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), 0, h->stream, h->d_model, P, xu, sol, goals,
-                         h->has_fext ? h->d_fext : nullptr, active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode);
   });
+}
+
+// Number of concurrent problem ranges for a batch of B.  The three kernels are latency-bound
+// with different bottlenecks (MFMA chains, fp64 VALU chains, loads); ranges on separate streams
+// let waves of different kernels share a SIMD.
+int chunks_for(const i7m_handle* h, int B) {
+  int c = h->chunks;
+  if (c <= 0) c = 1;  // measured: 2-4 ranges give no gain at B = 4096
+  c = std::min(c, I7M_MAX_CHUNKS);
+  while (c > 1 && B / c < 256) --c;
+  return c;
 }
 
 // The SQP loop on device buffers (xu updated in place).
 int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double* d_goals, int goal_stride,
             ProblemStats* d_st) {
-  SolveParams P = params_of(h, B, goal_stride);
   HIPCHK(hipMemsetAsync(d_st, 0, sizeof(ProblemStats) * (size_t)B, h->stream));
   // all problems start active
   HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->d_active), 1, (size_t)B, h->stream));
+  const int C = chunks_for(h, B);
+  const long N = h->cfg.N, T = 18 * N - 6;
+  hipStream_t ss[I7M_MAX_CHUNKS];
+  int b0[I7M_MAX_CHUNKS + 1];
+  for (int c = 0; c <= C; ++c) b0[c] = (int)((long)B * c / C);
+  if (C == 1) {
+    ss[0] = h->stream;
+  } else {  // fork: every worker stream waits for the caller's stream
+    HIPCHK(hipEventRecord(h->fork, h->stream));
+    for (int c = 0; c < C; ++c) {
+      ss[c] = h->workers[c];
+      HIPCHK(hipStreamWaitEvent(ss[c], h->fork, 0));
+    }
+  }
   for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
-    int rc;
-    if ((rc = launch_linearize(h, P, d_xu, d_goals, h->d_active))) return rc;
-    if ((rc = launch_riccati(h, P, d_xu, d_xs, h->d_active, h->d_sol))) return rc;
-    if ((rc = launch_linesearch(h, P, d_xu, h->d_sol, d_goals, h->d_active, d_st, nullptr, it, 0))) return rc;
+    for (int c = 0; c < C; ++c) {
+      const long o = b0[c];
+      const Bufs W = bufs_at(h, o);
+      SolveParams P = params_of(h, b0[c + 1] - b0[c], goal_stride);
+      double* xu = d_xu + o * T;
+      const double* xs = d_xs + o * 12;
+      const double* g = d_goals + o * N * goal_stride;
+      int* act = h->d_active + o;
+      int rc;
+      if ((rc = launch_linearize(h, ss[c], W, P, xu, g, act))) return rc;
+      if ((rc = launch_riccati(h, ss[c], W, P, xu, xs, act, h->d_sol + o * T))) return rc;
+      if ((rc = launch_linesearch(h, ss[c], W, P, xu, h->d_sol + o * T, g, act, d_st + o, nullptr, it, 0))) return rc;
+    }
+  }
+  if (C > 1) {  // join
+    for (int c = 0; c < C; ++c) {
+      HIPCHK(hipEventRecord(h->join[c], ss[c]));
+      HIPCHK(hipStreamWaitEvent(h->stream, h->join[c], 0));
+    }
   }
   return I7M_OK;
 }
@@ -303,6 +362,13 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   // developer knob for A/B profiling of the two QP kernels (default: MFMA)
   if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
   if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
+  if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
+  for (int c = 0; c < I7M_MAX_CHUNKS; ++c)
+    if (hipStreamCreateWithFlags(&h->workers[c], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->join[c], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(I7M_EHIP, "worker stream creation failed"));
+  if (hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(I7M_EHIP, "event creation failed"));
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
   // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
   const size_t scratch = std::max(Bm * T, (size_t)256 * 114);
@@ -343,6 +409,14 @@ void i7m_destroy(i7m_handle* h) {
     hipEventDestroy(t.b);
   }
   for (auto e : h->pool) hipEventDestroy(e);
+  for (int c = 0; c < I7M_MAX_CHUNKS; ++c) {
+    if (h->workers[c]) {
+      hipStreamSynchronize(h->workers[c]);
+      hipStreamDestroy(h->workers[c]);
+    }
+    if (h->join[c]) hipEventDestroy(h->join[c]);
+  }
+  if (h->fork) hipEventDestroy(h->fork);
   if (h->own) hipStreamDestroy(h->own);
   delete h;
 }
@@ -419,8 +493,8 @@ int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = launch_linearize(h, P, h->d_xu, h->d_goal, nullptr))) return rc;
-  if ((rc = launch_riccati(h, P, h->d_xu, h->d_xs, nullptr, h->d_sol))) return rc;
+  if ((rc = launch_linearize(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_goal, nullptr))) return rc;
+  if ((rc = launch_riccati(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol))) return rc;
   if ((rc = copy_out(h, sol, h->d_sol, (size_t)B * T))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
@@ -437,7 +511,7 @@ int i7m_linearize(i7m_handle* h, int32_t B, const double* xu, const double* goal
   SolveParams P = params_of(h, B, goal_stride);
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = launch_linearize(h, P, h->d_xu, h->d_goal, nullptr))) return rc;
+  if ((rc = launch_linearize(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_goal, nullptr))) return rc;
   if (lin && (rc = copy_out(h, lin, h->d_lin, (size_t)B * (N - 1) * LIN_STRIDE))) return rc;
   if (cost && (rc = copy_out(h, cost, h->d_cost, (size_t)B * N * COST_STRIDE))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -476,7 +550,7 @@ int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_sol, xu_full, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = launch_linesearch(h, P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1))) return rc;
+  if ((rc = launch_linesearch(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1))) return rc;
   if ((rc = copy_out(h, alpha, h->d_out, (size_t)B))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
