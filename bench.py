@@ -100,6 +100,45 @@ def _pmc_traffic(kernel: str, B: int, N: int):
         return None
 
 
+def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N: int = 64):
+    """SURVEY.md §8d config 4 (extension, no reference number): B problems, N knots, box rows on
+    q, v, u (URDF limits), interior-point QP mode (I7M_QP_BOX).  Device-resident inputs, same
+    step definition as the headline; reported as an extra object, not as `value`."""
+    import torch
+    from indy7_mpc_amd import _lib
+    from indy7_mpc_amd.synthetic import make_batch
+
+    dev = torch.device("cuda", local)
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=_lib.QP_BOX)
+    h.set_stream(stream.cuda_stream)
+    xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 4)
+    t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
+    t_out = torch.empty_like(t_xu)
+
+    def step():
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    h.reset_kernel_times()
+    h.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    h.set_timing(False)
+    kt = h.kernel_times()
+    it, conv, _ = h.box_stats(B)
+    out = t_out.cpu().numpy()
+    return {"workload": f"config4: B={B}, N={N}, box rows on q/v/u (URDF limits), interior-point QP",
+            "value": B * steps / el, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
+            "ipm_iters_last_qp_mean": float(it.mean()), "ipm_converged_frac": float(conv.mean()),
+            "finite": bool(np.isfinite(out).all()),
+            "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +150,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=30)
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (box QP) extra object")
+    ap.add_argument("--config4-steps", type=int, default=3)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -208,6 +249,7 @@ def main():
     per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c,
                       "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)} for k, (ms, c) in ktimes.items()}
     cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads)
+    c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1)
     out = {
         "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
         "value": value,
@@ -249,6 +291,8 @@ def main():
                              "frac": value * fl["per_solve_mean"] / 1e12 / (FP64_PEAK_TFLOPS * world),
                              "flops_per_solve": fl["per_solve_mean"], "merit_evals_per_solve": fl["merit_evals_mean"]}
         out["cpu_baseline"] = cpu
+    if c4 is not None:
+        out["config4"] = c4
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

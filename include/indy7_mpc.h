@@ -15,7 +15,10 @@
  *                               step) for B independent problems, batch axis of
  *                               src/gato_mpc_batch.py:38-43,97-99
  *   i7m_qp                     OSQPSolver.setup_and_solve_qp  src/osqp_solver.py:137-143
- *                              (returns the QP minimiser sol.x, solved exactly)
+ *                              (returns the QP minimiser sol.x, solved exactly; with
+ *                               qp_mode = I7M_QP_BOX the QP also carries box rows on q, v, u
+ *                               — SURVEY.md §8d config 4, an extension without a reference
+ *                               counterpart; see oracle/box_ipm.py for its definition)
  *   i7m_linearize              update_constraint_matrix + update_cost_matrix
  *                                                             src/osqp_solver.py:70-135
  *   i7m_merit                  SQP_OSQP.eepos_cost + integrator_err
@@ -58,6 +61,11 @@ extern "C" {
 #define I7M_ENOMEM -3   /* device allocation failed */
 #define I7M_ENODEV -4   /* no usable gfx950 device */
 
+enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1 };
+#define I7M_BOX_Q 1     /* q_lower <= q <= q_upper    description/indy7.urdf:203-238 <limit> */
+#define I7M_BOX_V 2     /* |v| <= velocity limit */
+#define I7M_BOX_U 4     /* |u| <= effort limit */
+
 /* 6-DOF serial chain of revolute joints about local +z. Layout == RobotModel.packed(). */
 typedef struct i7m_model {
   double placement_R[6][9];   /* joint frame in parent joint frame, row-major */
@@ -68,8 +76,6 @@ typedef struct i7m_model {
   double gravity[3];          /* (0,0,-9.81), src/osqp_mpc.py:8-9 */
   double q_lower[6], q_upper[6], v_limit[6], effort_limit[6];
 } i7m_model;
-
-enum { I7M_QP_DIRECT = 0 };
 
 typedef struct i7m_config {
   int32_t N;            /* knot points (<= I7M_MAX_N), default 32   src/osqp_solver.py:7 */
@@ -84,8 +90,13 @@ typedef struct i7m_config {
   int32_t max_sqp_iters;/* 2                          src/osqp_sqp.py:77 */
   int32_t max_batch;    /* device buffers are sized for this many problems */
   int32_t device_id;
-  int32_t qp_mode;      /* I7M_QP_DIRECT: exact block-tridiagonal (Riccati) KKT solve */
+  int32_t qp_mode;      /* I7M_QP_DIRECT: exact block-tridiagonal (Riccati) KKT solve;
+                           I7M_QP_BOX: + box rows on q, v, u (interior point, Riccati Newton steps) */
   i7m_model model;
+  /* I7M_QP_BOX only (appended: the offsets above are unchanged) */
+  int32_t box_mask;     /* which rows: I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U (default all) */
+  int32_t box_max_iters;/* interior-point iterations per QP, default 30 */
+  double box_tol;       /* stop when mu < tol and the residuals shrank by tol, default 1e-8 */
 } i7m_config;
 
 /* Per-problem SQP statistics (keys of SQP_OSQP.stats, src/osqp_sqp.py:7-11). */
@@ -129,6 +140,11 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
 int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals,
            int32_t goal_stride, double* sol);
 
+/* I7M_QP_BOX: interior-point record of the most recent QP of problems [0, B) (the last
+ * i7m_qp, or the last SQP iteration of i7m_solve): corrector steps taken, 1 if converged
+ * (mu < box_tol and residuals reduced by box_tol), final mu.  Any output may be NULL. */
+int i7m_get_box_stats(i7m_handle* h, int32_t B, int32_t* iters, int32_t* converged, double* mu);
+
 /* Raw linearisation at xu.  lin (B, N-1, 114): per knot Aq(6x6,row-major, =dt*da/dq),
  * Av (=I+dt*da/dv), Bu (=dt*Minv), a (=ABA(q,v,u)); cost (B, N, 10): j = J^T e (6),
  * Qm, dQm, Rm, |e|.  Either output may be NULL. */
@@ -154,7 +170,7 @@ int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
             const double* fext, double* q_out, double* v_out);
 
 /* Per-kernel device timing with HIP events on the launch stream. */
-enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_COUNT = 3 };
+enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_COUNT = 5 };
 int i7m_set_timing(i7m_handle* h, int enable);
 /* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
 int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);

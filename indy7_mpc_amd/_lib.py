@@ -25,8 +25,8 @@ MAX_SQP = 8
 MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
-I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_COUNT = 0, 1, 2, 3
-KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch")
+I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_COUNT = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm")
 
 
 class I7MError(RuntimeError):
@@ -64,7 +64,14 @@ class i7m_config(C.Structure):
         ("device_id", C.c_int32),
         ("qp_mode", C.c_int32),
         ("model", i7m_model),
+        ("box_mask", C.c_int32),
+        ("box_max_iters", C.c_int32),
+        ("box_tol", C.c_double),
     ]
+
+
+QP_DIRECT, QP_BOX = 0, 1
+BOX_Q, BOX_V, BOX_U = 1, 2, 4
 
 
 class i7m_problem_stats(C.Structure):
@@ -102,6 +109,7 @@ SIGNATURES = [
     ("i7m_solve_device", C.c_int, [_H, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                    C.c_void_p]),
     ("i7m_qp", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
+    ("i7m_get_box_stats", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _DP]),
     ("i7m_linearize", C.c_int, [_H, C.c_int32, _DP, _DP, C.c_int32, _DP, _DP]),
     ("i7m_merit", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_linesearch", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
@@ -167,13 +175,15 @@ class Handle:
     """One device handle (= one OSQPSolver-like solver state on one GPU)."""
 
     def __init__(self, model, N=32, dt=0.01, dQ_cost=0.01, R_cost=1e-5, QN_cost=100.0, regularize=True, eps=1.0,
-                 max_batch=1, device_id=0, mu=10.0, step_tol=1e-3, max_sqp_iters=2):
+                 max_batch=1, device_id=0, mu=10.0, step_tol=1e-3, max_sqp_iters=2, qp_mode=QP_DIRECT,
+                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8):
         lib = load()
         cfg = i7m_config()
         _check(lib.i7m_config_default(C.byref(cfg)))
         cfg.N, cfg.dt, cfg.dQ_cost, cfg.R_cost, cfg.QN_cost = int(N), float(dt), float(dQ_cost), float(R_cost), float(QN_cost)
         cfg.regularize, cfg.eps, cfg.mu, cfg.step_tol = int(bool(regularize)), float(eps), float(mu), float(step_tol)
         cfg.max_sqp_iters, cfg.max_batch, cfg.device_id = int(max_sqp_iters), int(max_batch), int(device_id)
+        cfg.qp_mode, cfg.box_mask, cfg.box_max_iters, cfg.box_tol = int(qp_mode), int(box_mask), int(box_max_iters), float(box_tol)
         packed = np.ascontiguousarray(model.packed(), dtype=np.float64)
         assert packed.nbytes == C.sizeof(i7m_model), (packed.nbytes, C.sizeof(i7m_model))
         C.memmove(C.byref(cfg.model), packed.ctypes.data, packed.nbytes)
@@ -238,6 +248,15 @@ class Handle:
         sol = np.empty_like(xu)
         _check(self._lib.i7m_qp(self._h, B, _ptr(xu), _ptr(xc), _ptr(goals), stride, _ptr(sol)))
         return sol
+
+    def box_stats(self, B):
+        """Interior-point record of the last QP (box mode): (iters, converged, mu), each (B,)."""
+        it = np.zeros(B, dtype=np.int32)
+        cv = np.zeros(B, dtype=np.int32)
+        mu = np.zeros(B)
+        ip = C.POINTER(C.c_int32)
+        _check(self._lib.i7m_get_box_stats(self._h, int(B), it.ctypes.data_as(ip), cv.ctypes.data_as(ip), _ptr(mu)))
+        return it, cv.astype(bool), mu
 
     def linearize(self, xu, goals):
         xu, goals, B, stride = self._batch(xu, goals)
@@ -317,7 +336,7 @@ class Handle:
         ms = (C.c_double * I7M_K_COUNT)()
         cnt = (C.c_int32 * I7M_K_COUNT)()
         _check(self._lib.i7m_get_kernel_times(self._h, ms, cnt, I7M_K_COUNT))
-        return {KERNEL_NAMES[i]: (ms[i], cnt[i]) for i in range(I7M_K_COUNT)}
+        return {KERNEL_NAMES[i]: (ms[i], cnt[i]) for i in range(I7M_K_COUNT) if cnt[i] > 0}
 
     def reset_kernel_times(self):
         _check(self._lib.i7m_reset_kernel_times(self._h))

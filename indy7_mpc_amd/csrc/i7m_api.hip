@@ -19,6 +19,7 @@
 #include "i7m_linearize.h"
 #include "i7m_riccati.h"
 #include "i7m_riccati_mfma.h"
+#include "i7m_box.h"
 
 using namespace i7m;
 
@@ -60,6 +61,10 @@ struct i7m_handle {
   int* d_active = nullptr;
   ProblemStats* d_stats = nullptr;
   double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
+  // I7M_QP_BOX (i7m_box.h): iterate, bound duals, Riccati inputs, predictor step; (max_batch, T)
+  double *d_bx = nullptr, *d_bzl = nullptr, *d_bzu = nullptr, *d_bsig = nullptr, *d_bh = nullptr, *d_bdxa = nullptr;
+  IpmState* d_bst = nullptr;
+  int* d_bact = nullptr;
   uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
   int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
   int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
@@ -74,8 +79,8 @@ struct i7m_handle {
   bool timing = false;
   std::vector<Timing> ev;
   std::vector<hipEvent_t> pool;
-  double ms_sum[I7M_K_COUNT] = {0, 0, 0};
-  int counts[I7M_K_COUNT] = {0, 0, 0};
+  double ms_sum[I7M_K_COUNT] = {};
+  int counts[I7M_K_COUNT] = {};
 };
 
 namespace {
@@ -170,12 +175,28 @@ struct Bufs {
   double* cost;
   double* kbuf;
   const double* fext;  // nullptr: no external wrench
+  // box mode only (nullptr otherwise)
+  double *bx, *bzl, *bzu, *bsig, *bh, *bdxa;
+  IpmState* bst;
+  int* bact;
 };
 
 Bufs bufs_at(const i7m_handle* h, long b0) {
-  const long N = h->cfg.N;
-  return {h->d_lin + b0 * (N - 1) * LIN_STRIDE, h->d_cost + b0 * N * COST_STRIDE,
-          h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr};
+  const long N = h->cfg.N, T = 18 * N - 6;
+  Bufs W{h->d_lin + b0 * (N - 1) * LIN_STRIDE, h->d_cost + b0 * N * COST_STRIDE,
+         h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr,
+         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (h->cfg.qp_mode == I7M_QP_BOX) {
+    W.bx = h->d_bx + b0 * T;
+    W.bzl = h->d_bzl + b0 * T;
+    W.bzu = h->d_bzu + b0 * T;
+    W.bsig = h->d_bsig + b0 * T;
+    W.bh = h->d_bh + b0 * T;
+    W.bdxa = h->d_bdxa + b0 * T;
+    W.bst = h->d_bst + b0;
+    W.bact = h->d_bact + b0;
+  }
+  return W;
 }
 
 int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
@@ -226,6 +247,54 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
   });
 }
 
+BoxParams box_params(const i7m_handle* h) {
+  BoxParams BP;
+  BP.mask = h->cfg.box_mask;
+  BP.max_iters = h->cfg.box_max_iters;
+  BP.tol = h->cfg.box_tol;
+  BP.theta = 0.01;
+  BP.eta = 0.99;
+  return BP;
+}
+
+// The QP of one SQP iteration: the exact equality-constrained solve (k_riccati_mfma), and in
+// box mode the interior-point iteration started from it (i7m_box.h; oracle/box_ipm.py).
+// Returns where the minimiser is: `sol`, or W.bx in box mode.
+int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu, const double* xs,
+             const int* active, double* sol, const double** out) {
+  int rc;
+  if ((rc = launch_riccati(h, s, W, P, xu, xs, active, sol))) return rc;
+  *out = sol;
+  if (h->cfg.qp_mode != I7M_QP_BOX || P.B == 0) return I7M_OK;
+  const BoxParams BP = box_params(h);
+  const dim3 g(P.B), blk(64);
+  rc = timed(h, s, I7M_K_IPM, [&] {
+    hipLaunchKernelGGL(k_ipm_init, g, blk, 0, s, h->d_model, P, BP, sol, active, W.bx, W.bzl, W.bzu, W.bsig, W.bh,
+                       W.bst, W.bact);
+  });
+  if (rc) return rc;
+  for (int it = 0; it < BP.max_iters; ++it) {
+    for (int half = 0; half < 2; ++half) {
+      rc = timed(h, s, I7M_K_RICCATI_BOX, [&] {
+        hipLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, P, xu, xs, W.lin, W.cost, W.bact, W.kbuf, sol,
+                           W.bsig, W.bh);
+      });
+      if (rc) return rc;
+      rc = timed(h, s, I7M_K_IPM, [&] {
+        if (half == 0)
+          hipLaunchKernelGGL(k_ipm_pred, g, blk, 0, s, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bh,
+                             W.bst, W.bact);
+        else
+          hipLaunchKernelGGL(k_ipm_corr, g, blk, 0, s, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bsig,
+                             W.bh, W.bst, W.bact);
+      });
+      if (rc) return rc;
+    }
+  }
+  *out = W.bx;
+  return I7M_OK;
+}
+
 // Number of concurrent problem ranges for a batch of B.  The three kernels are latency-bound
 // with different bottlenecks (MFMA chains, fp64 VALU chains, loads); ranges on separate streams
 // let waves of different kernels share a SIMD.
@@ -268,8 +337,9 @@ int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double
       int* act = h->d_active + o;
       int rc;
       if ((rc = launch_linearize(h, ss[c], W, P, xu, g, act))) return rc;
-      if ((rc = launch_riccati(h, ss[c], W, P, xu, xs, act, h->d_sol + o * T))) return rc;
-      if ((rc = launch_linesearch(h, ss[c], W, P, xu, h->d_sol + o * T, g, act, d_st + o, nullptr, it, 0))) return rc;
+      const double* qsol = nullptr;
+      if ((rc = solve_qp(h, ss[c], W, P, xu, xs, act, h->d_sol + o * T, &qsol))) return rc;
+      if ((rc = launch_linesearch(h, ss[c], W, P, xu, qsol, g, act, d_st + o, nullptr, it, 0))) return rc;
     }
   }
   if (C > 1) {  // join
@@ -328,6 +398,9 @@ int i7m_config_default(i7m_config* c) {
   c->max_batch = 1;
   c->device_id = 0;
   c->qp_mode = I7M_QP_DIRECT;
+  c->box_mask = I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U;
+  c->box_max_iters = 30;
+  c->box_tol = 1e-8;
   return I7M_OK;
 }
 
@@ -337,7 +410,12 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (cfg->N < 2 || cfg->N > I7M_MAX_N) return fail(I7M_EINVAL, "N must be in [2, 64]");
   if (cfg->max_batch < 1) return fail(I7M_EINVAL, "max_batch must be >= 1");
   if (cfg->max_sqp_iters < 1 || cfg->max_sqp_iters > I7M_MAX_SQP) return fail(I7M_EINVAL, "max_sqp_iters in [1, 8]");
-  if (cfg->qp_mode != I7M_QP_DIRECT) return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (cfg->qp_mode != I7M_QP_DIRECT && cfg->qp_mode != I7M_QP_BOX) return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (cfg->qp_mode == I7M_QP_BOX) {
+    if (cfg->box_mask < 0 || cfg->box_mask > 7) return fail(I7M_EINVAL, "box_mask must be a subset of Q|V|U (0..7)");
+    if (cfg->box_max_iters < 1 || cfg->box_max_iters > 200) return fail(I7M_EINVAL, "box_max_iters in [1, 200]");
+    if (!(cfg->box_tol > 0.0)) return fail(I7M_EINVAL, "box_tol must be > 0");
+  }
   if (!(cfg->dt > 0.0)) return fail(I7M_EINVAL, "dt must be > 0");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -381,6 +459,11 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_out, scratch * 8) &&
             alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
             alloc((void**)&h->d_fext, Bm * 6 * 8) && alloc((void**)&h->d_ric_desc, RIC_DESC_WORDS * 4);
+  if (ok && cfg->qp_mode == I7M_QP_BOX)
+    ok = alloc((void**)&h->d_bx, Bm * T * 8) && alloc((void**)&h->d_bzl, Bm * T * 8) &&
+         alloc((void**)&h->d_bzu, Bm * T * 8) && alloc((void**)&h->d_bsig, Bm * T * 8) &&
+         alloc((void**)&h->d_bh, Bm * T * 8) && alloc((void**)&h->d_bdxa, Bm * T * 8) &&
+         alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
   std::vector<uint32_t> desc(RIC_DESC_WORDS);
   build_riccati_desc(desc.data());
@@ -401,7 +484,8 @@ void i7m_destroy(i7m_handle* h) {
   hipSetDevice(h->dev);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc};
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc,
+                  h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& t : h->ev) {
@@ -494,9 +578,26 @@ int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
   if ((rc = launch_linearize(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_goal, nullptr))) return rc;
-  if ((rc = launch_riccati(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol))) return rc;
-  if ((rc = copy_out(h, sol, h->d_sol, (size_t)B * T))) return rc;
+  const double* qsol = nullptr;
+  if ((rc = solve_qp(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol, &qsol))) return rc;
+  if ((rc = copy_out(h, sol, qsol, (size_t)B * T))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_get_box_stats(i7m_handle* h, int32_t B, int32_t* iters, int32_t* converged, double* mu) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (h->cfg.qp_mode != I7M_QP_BOX) return fail(I7M_EINVAL, "handle is not in I7M_QP_BOX mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  HIPCHK(hipSetDevice(h->dev));
+  std::vector<IpmState> st((size_t)B);
+  if (B) HIPCHK(hipMemcpyAsync(st.data(), h->d_bst, sizeof(IpmState) * (size_t)B, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int b = 0; b < B; ++b) {
+    if (iters) iters[b] = st[b].iters;
+    if (converged) converged[b] = st[b].converged;
+    if (mu) mu[b] = st[b].mu;
+  }
   return I7M_OK;
 }
 

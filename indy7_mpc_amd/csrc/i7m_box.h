@@ -1,0 +1,235 @@
+// i7m_box.h — interior-point iteration of the box-constrained QP mode (I7M_QP_BOX, SURVEY.md
+// §8d config 4).  Restates oracle/box_ipm.py::ipm_box step by step; the Newton steps
+// themselves are k_riccati_mfma<0, true> (i7m_riccati_mfma.h) on the same linearisation.
+//
+// One wavefront per problem, lanes strided over the T = 18N-6 trajectory entries.  Per
+// problem, in (B, T) device arrays: the iterate x, the bound duals z_l / z_u, the Riccati
+// inputs Sigma / h, and the predictor step dx_aff; and in IpmState the scalars.
+// Slacks s_l = x - lo, s_u = hi - x are recomputed from x (never stored).
+#pragma once
+
+#include "i7m_kernels.h"
+
+namespace i7m {
+
+struct BoxParams {
+  int mask;       // I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U
+  int max_iters;
+  double tol;
+  double theta;   // initial interior margin, fraction of the box width
+  double eta;     // step-to-boundary fraction
+};
+
+struct IpmState {
+  double mu, rfrac, smu;  // complementarity, prod(1 - alpha), sigma * mu of the corrector
+  int iters, nb;          // corrector steps taken, bounded entries
+  int converged, pad;
+};
+
+// Bounds of trajectory entry e (knot e / 18, slot e % 18); false if unbounded.  The initial
+// state is fixed by the equality rows and never bounded (oracle/box_ipm.py::box_bounds).
+__device__ __forceinline__ bool box_of(const DevModel& M, int mask, int e, double& lo, double& hi) {
+  const int k = e / 18, j = e - 18 * (e / 18);
+  if (k == 0 && j < 12) return false;
+  if (j < 6) {
+    if (!(mask & 1)) return false;
+    lo = M.qlo[j];
+    hi = M.qhi[j];
+  } else if (j < 12) {
+    if (!(mask & 2)) return false;
+    hi = M.vlim[j - 6];
+    lo = -hi;
+  } else {
+    if (!(mask & 4)) return false;
+    hi = M.ulim[j - 12];
+    lo = -hi;
+  }
+  return true;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+// the largest t <= 1 with v + t dv >= 0 (v > 0), folded into a running minimum
+__device__ __forceinline__ double ratio_min(double t, double v, double dv) {
+  return (dv < 0.0) ? fmin(t, -v / dv) : t;
+}
+
+// x = clip(x_eq) into the interior, z = 1, mu, and the first predictor's Sigma and h.
+__global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ xeq, const int* __restrict__ active,
+                                                 double* __restrict__ x, double* __restrict__ zl, double* __restrict__ zu,
+                                                 double* __restrict__ sig, double* __restrict__ h,
+                                                 IpmState* __restrict__ st, int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  const int l = threadIdx.x;
+  const DevModel& M = *Mg;
+  const long o = (long)b * P.T;
+  double acc = 0.0;
+  int nb = 0;
+  for (int e = l; e < P.T; e += 64) {
+    double lo, hi, xv = xeq[o + e], z = 0.0, s = 0.0;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double w = hi - lo;
+      xv = fmin(fmax(xv, lo + BP.theta * w), hi - BP.theta * w);
+      z = 1.0;
+      const double sl = xv - lo, su = hi - xv;
+      acc += sl + su;
+      s = 1.0 / sl + 1.0 / su;
+      ++nb;
+    }
+    x[o + e] = xv;
+    zl[o + e] = z;
+    zu[o + e] = z;
+    sig[o + e] = s;
+    h[o + e] = -s * xv;
+  }
+  acc = wave_sum(acc);
+  nb = wave_isum(nb);
+  if (l == 0) {
+    IpmState S;
+    S.mu = nb ? acc / (2.0 * nb) : 0.0;
+    S.rfrac = 1.0;
+    S.smu = 0.0;
+    S.iters = 0;
+    S.nb = nb;
+    S.converged = (nb == 0);
+    S.pad = 0;
+    st[b] = S;
+    ipm_active[b] = (active ? active[b] : 1) && nb > 0;
+  }
+}
+
+// Predictor: dx_aff = y - x; affine step lengths and mu_aff; sigma*mu; the corrector's h.
+__global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ y, const double* __restrict__ x,
+                                                 const double* __restrict__ zl, const double* __restrict__ zu,
+                                                 double* __restrict__ dxa, double* __restrict__ h,
+                                                 IpmState* __restrict__ st, const int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B || !ipm_active[b]) return;
+  const int l = threadIdx.x;
+  const DevModel& M = *Mg;
+  const long o = (long)b * P.T;
+  double ap = 1.0, ad = 1.0;
+  for (int e = l; e < P.T; e += 64) {
+    const double d = y[o + e] - x[o + e];
+    dxa[o + e] = d;
+    double lo, hi;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
+      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+      ap = ratio_min(ratio_min(ap, sl, d), su, -d);
+      ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
+    }
+  }
+  ap = wave_min(ap);
+  ad = wave_min(ad);
+  double acc = 0.0;
+  for (int e = l; e < P.T; e += 64) {
+    double lo, hi;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double d = dxa[o + e], xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
+      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+      acc += (sl + ap * d) * (a + ad * dzl) + (su - ap * d) * (c + ad * dzu);
+    }
+  }
+  acc = wave_sum(acc);
+  IpmState S = st[b];
+  const double mua = acc / (2.0 * S.nb);
+  const double r = mua / S.mu;
+  const double smu = r * r * r * S.mu;
+  for (int e = l; e < P.T; e += 64) {
+    double lo, hi, hv = 0.0;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double d = dxa[o + e], xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
+      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+      const double rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
+      const double s = a / sl + c / su;
+      hv = -a + c + (rl / sl - ru / su) - s * xv;
+    }
+    h[o + e] = hv;
+  }
+  if (l == 0) st[b].smu = smu;
+}
+
+// Corrector: dx = y - x, common step, update (x, z_l, z_u), new mu, convergence, and the next
+// predictor's Sigma and h.
+__global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ y, double* __restrict__ x,
+                                                 double* __restrict__ zl, double* __restrict__ zu,
+                                                 const double* __restrict__ dxa, double* __restrict__ sig,
+                                                 double* __restrict__ h, IpmState* __restrict__ st,
+                                                 int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B || !ipm_active[b]) return;
+  const int l = threadIdx.x;
+  const DevModel& M = *Mg;
+  const long o = (long)b * P.T;
+  const double smu = st[b].smu;
+  double t = 1.0;
+  for (int e = l; e < P.T; e += 64) {
+    double lo, hi;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double d = y[o + e] - x[o + e], da = dxa[o + e];
+      const double xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
+      const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+      const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+      const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
+      t = ratio_min(ratio_min(t, sl, d), su, -d);
+      t = ratio_min(ratio_min(t, a, dzl), c, dzu);
+    }
+  }
+  t = wave_min(t);
+  const double al = fmin(1.0, BP.eta * t);
+  double acc = 0.0;
+  for (int e = l; e < P.T; e += 64) {
+    const double d = y[o + e] - x[o + e];
+    const double xv = x[o + e];
+    double lo, hi;
+    if (box_of(M, BP.mask, e, lo, hi)) {
+      const double da = dxa[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
+      const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+      const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+      const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
+      const double xn = xv + al * d, an = a + al * dzl, cn = c + al * dzu;
+      x[o + e] = xn;
+      zl[o + e] = an;
+      zu[o + e] = cn;
+      const double sln = xn - lo, sun = hi - xn;
+      acc += sln * an + sun * cn;
+      const double s = an / sln + cn / sun;
+      sig[o + e] = s;
+      h[o + e] = -s * xn;
+    } else {
+      x[o + e] = xv + al * d;
+      sig[o + e] = 0.0;
+      h[o + e] = 0.0;
+    }
+  }
+  acc = wave_sum(acc);
+  if (l == 0) {
+    IpmState S = st[b];
+    S.mu = acc / (2.0 * S.nb);
+    S.rfrac *= 1.0 - al;
+    S.iters += 1;
+    S.converged = (S.mu < BP.tol && S.rfrac < BP.tol);
+    st[b] = S;
+    if (S.converged || S.iters >= BP.max_iters) ipm_active[b] = 0;
+  }
+}
+
+}  // namespace i7m

@@ -24,21 +24,25 @@ namespace i7m {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 enum : int {
-  MO_AQ = 0,     // stage stash: Aq(36) Av(36) Bu(36) a(6) | cost(10) | XU_k(18)  = 142
+  MO_AQ = 0,     // stage stash: Aq(36) Av(36) Bu(36) a(6) | cost(10) | XU_k(18) | [BOX: Sigma(18) h(18)]
   MO_AV = 36,
   MO_BU = 72,
   MO_A = 108,
   MO_W = 114,    // j(6) Qm dQm Rm |e|
   MO_X = 124,
-  MO_CV = 142,   // 6
-  MO_RU = 148,   // 6   Rm u
-  MO_QV = 154,   // 12  Qm j | dQm v
-  MO_H = 166,    // 36
-  MO_G = 202,    // 78  G~ (6 x 13)
-  MO_KT = 280,   // 78  K~ (6 x 13)
-  MO_ZERO = 358,
-  MO_ONE = 359,
-  MO_TOTAL = 360,
+  MO_SIG = 142,  // BOX: interior-point diagonal Sigma of the knot (q v u)
+  MO_HB = 160,   // BOX: linear-term shift h of the knot (q v u)
+  MO_CV = 178,   // 6
+  MO_RU = 184,   // 6   Rm u (+ h_u)
+  MO_QV = 190,   // 12  Qm j | dQm v
+  MO_LIN = 202,  // 12  BOX: linear state terms QV + h_x
+  MO_RD = 214,   // 6   BOX: R diagonal Rm + Sigma_u
+  MO_H = 220,    // 36
+  MO_G = 256,    // 78  G~ (6 x 13)
+  MO_KT = 334,   // 78  K~ (6 x 13)
+  MO_ZERO = 412,
+  MO_ONE = 413,
+  MO_TOTAL = 414,
 };
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -62,13 +66,19 @@ __device__ __forceinline__ double rcp_nr(double d) {
 
 // ABL (diagnostic builds only, results invalid): bit 0 skips the forward rollout, bit 1
 // replaces the Gauss-Jordan solve by a scaling; used to split the kernel's time.
+// BOX: the interior-point Newton step of the box-constrained QP (oracle/box_ipm.py): the same
+// QP with Hessian P + diag(Sigma) and linear term g + h, Sigma and h given per variable in
+// bsig / bh (B, T).  The equality rows are unchanged, so the result is the Newton iterate
+// x + dx itself.
 // 4 waves/SIMD (<= 128 VGPRs, MFMA accumulators in VGPRs): B = 4096 single-wave problems fit the
 // 1024 SIMDs in one round.
-template <int ABL>
+template <int ABL, bool BOX = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
                                                      const double* __restrict__ xs, const double* __restrict__ lin,
                                                      const double* __restrict__ cost, const int* __restrict__ active,
-                                                     double* __restrict__ kbuf, double* __restrict__ sol) {
+                                                     double* __restrict__ kbuf, double* __restrict__ sol,
+                                                     const double* __restrict__ bsig = nullptr,
+                                                     const double* __restrict__ bh = nullptr) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
@@ -108,7 +118,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     offB[s - 1] = (k >= 6 && lr < 6) ? MO_BU + 6 * (k - 6) + lr : MO_ZERO;
   }
   // Q~[lq+4i][lr] = sh[q1[i]] * sh[q2[i]];  R on the u diagonal;  N~ = r in column 12
-  int q1[4], q2[4], oR[4], oN[4];
+  // BOX: + Sigma on the state diagonal (oS), linear column from MO_LIN, R diagonal from MO_RD
+  constexpr int LINC = BOX ? MO_LIN : MO_QV;
+  int q1[4], q2[4], oR[4], oN[4], oS[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = lq + 4 * i, c = lr;
@@ -116,10 +128,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     q2[i] = MO_ZERO;
     if (r < 6 && c < 6) { q1[i] = MO_QV + r; q2[i] = MO_W + c; }
     else if (r >= 6 && r < 12 && r == c) { q1[i] = MO_W + 7; q2[i] = MO_ONE; }
-    else if (r < 12 && c == 12) { q1[i] = MO_QV + r; q2[i] = MO_ONE; }
-    else if (r == 12 && c < 12) { q1[i] = MO_QV + c; q2[i] = MO_ONE; }
-    oR[i] = (r == c && r < 6) ? MO_W + 8 : MO_ZERO;
+    else if (r < 12 && c == 12) { q1[i] = LINC + r; q2[i] = MO_ONE; }
+    else if (r == 12 && c < 12) { q1[i] = LINC + c; q2[i] = MO_ONE; }
+    oR[i] = (r == c && r < 6) ? (BOX ? MO_RD + r : MO_W + 8) : MO_ZERO;
     oN[i] = (c == 12 && r < 6) ? MO_RU + r : MO_ZERO;
+    oS[i] = (BOX && r == c && r < 12) ? MO_SIG + r : MO_ZERO;
   }
   // K~[4s+lq][lr] for s = 0, 1
   int oK[2];
@@ -132,27 +145,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   // ---- terminal cost-to-go V~ = Q~_{N-1}
   if (l < COST_STRIDE) sh[MO_W + l] = CB[(N - 1) * COST_STRIDE + l];
   if (l < 12) sh[MO_X + l] = X[18 * (N - 1) + l];
+  if (BOX && l < 12) {
+    sh[MO_SIG + l] = bsig[(long)b * P.T + 18 * (N - 1) + l];
+    sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
+  }
   if (l == 0) { sh[MO_ZERO] = 0.0; sh[MO_ONE] = 1.0; }
   __syncthreads();
-  if (l < 12) sh[MO_QV + l] = (l < 6) ? sh[MO_W + 6] * sh[MO_W + l] : sh[MO_W + 7] * sh[MO_X + l];
+  if (l < 12) {
+    const double qv = (l < 6) ? sh[MO_W + 6] * sh[MO_W + l] : sh[MO_W + 7] * sh[MO_X + l];
+    sh[MO_QV + l] = qv;
+    if (BOX) sh[MO_LIN + l] = qv + sh[MO_HB + l];
+  }
   __syncthreads();
   d4 V;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) V[i] = sh[q1[i]] * sh[q2[i]];
+  for (int i = 0; i < 4; ++i) V[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
 
+  constexpr int SE = BOX ? 178 : 142;  // stash length
   auto src = [&](int k, int e) -> const double* {
     if (e < LIN_STRIDE) return LINb + (long)k * LIN_STRIDE + e;
     if (e < LIN_STRIDE + COST_STRIDE) return CB + k * COST_STRIDE + (e - LIN_STRIDE);
-    return X + 18 * k + (e - LIN_STRIDE - COST_STRIDE);
+    if (!BOX || e < 142) return X + 18 * k + (e - LIN_STRIDE - COST_STRIDE);
+    if (e < 160) return bsig + (long)b * P.T + 18 * k + (e - 142);
+    return bh + (long)b * P.T + 18 * k + (e - 160);
   };
-  const int e2 = (l + 128 < 142) ? l + 128 : 141;
+  const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
   double p0 = *src(N - 2, l), p1 = *src(N - 2, l + 64), p2 = *src(N - 2, e2);
 
   for (int k = N - 2; k >= 0; --k) {
     __syncthreads();
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
-    if (l + 128 < 142) sh[MO_AQ + l + 128] = p2;
+    if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
     __syncthreads();
     if (k > 0) { p0 = *src(k - 1, l); p1 = *src(k - 1, l + 64); p2 = *src(k - 1, e2); }
     if (l < 6) {  // c_v = v + dt a - (Aq q + Av v + Bu u)   (src/osqp_solver.py:76-81)
@@ -163,10 +187,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
                sh[MO_BU + 6 * l + jj] * sh[MO_X + 12 + jj];
       sh[MO_CV + l] = (sh[MO_X + 6 + l] + sh[MO_A + l] * dt) - acc;
     } else if (l < 12) {
-      sh[MO_RU + l - 6] = sh[MO_W + 8] * sh[MO_X + 12 + (l - 6)];
+      sh[MO_RU + l - 6] = sh[MO_W + 8] * sh[MO_X + 12 + (l - 6)] + (BOX ? sh[MO_HB + 12 + (l - 6)] : 0.0);
+      if (BOX) sh[MO_RD + l - 6] = sh[MO_W + 8] + sh[MO_SIG + 12 + (l - 6)];
     } else if (l < 24) {
       const int r = l - 12;
-      sh[MO_QV + r] = (r < 6) ? sh[MO_W + 6] * sh[MO_W + r] : sh[MO_W + 7] * sh[MO_X + r];
+      const double qv = (r < 6) ? sh[MO_W + 6] * sh[MO_W + r] : sh[MO_W + 7] * sh[MO_X + r];
+      sh[MO_QV + r] = qv;
+      if (BOX) sh[MO_LIN + r] = qv + sh[MO_HB + r];
     }
     __syncthreads();
     double bA[4], bB[2];
@@ -177,7 +204,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     d4 Qi, Ri, Ni;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      Qi[i] = sh[q1[i]] * sh[q2[i]];
+      Qi[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
       Ri[i] = sh[oR[i]];
       Ni[i] = sh[oN[i]];
     }

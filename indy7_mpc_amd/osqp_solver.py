@@ -31,7 +31,11 @@ class QPSolution:
 
 class OSQPSolver:
     def __init__(self, model, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
-                 max_batch=1, device_id=0):
+                 max_batch=1, device_id=0, box_constraints=False, box_mask=_lib.BOX_Q | _lib.BOX_V | _lib.BOX_U,
+                 box_max_iters=30, box_tol=1e-8):
+        """Reference signature (src/osqp_solver.py:7) plus: max_batch / device_id (device
+        buffers), and the config-4 extension ``box_constraints``: box rows on
+        q, v, u from the model's URDF limits, solved by the interior-point mode (I7M_QP_BOX)."""
         self.model = model
         self.data = model.createData()
         self.N = N
@@ -58,8 +62,10 @@ class OSQPSolver:
                                          np.ones((self.nq, 2 * self.nq))])])
         self.B_k = np.zeros((self.nx, self.nq))
         self.cx_k = np.zeros(self.nx)
+        self.box = dict(qp_mode=_lib.QP_BOX if box_constraints else _lib.QP_DIRECT, box_mask=box_mask,
+                        box_max_iters=box_max_iters, box_tol=box_tol)
         self.handle = _lib.Handle(model, N=N, dt=dt, dQ_cost=dQ_cost, R_cost=R_cost, QN_cost=QN_cost,
-                                  regularize=regularize, eps=eps, max_batch=max_batch, device_id=device_id)
+                                  regularize=regularize, eps=eps, max_batch=max_batch, device_id=device_id, **self.box)
 
     # ---- sparsity templates (src/osqp_solver.py:48-68) -----------------------------------
     def initialize_P(self):

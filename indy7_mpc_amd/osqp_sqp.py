@@ -57,7 +57,7 @@ class SQP_OSQP:
             s = self.solver
             self._batch_handle = _lib.Handle(s.model, N=s.N, dt=s.dt, dQ_cost=s.dQ_cost, R_cost=s.R_cost,
                                              QN_cost=s.QN_cost, regularize=s.regularize, eps=s.eps, max_batch=B,
-                                             device_id=h.cfg.device_id)
+                                             device_id=h.cfg.device_id, **s.box)
         return self._batch_handle
 
     def sqp_batch(self, xcur_batch, eepos_goals_batch, XU_batch):

@@ -44,7 +44,7 @@ class OSQPSolverRef:
     """Restates OSQPSolver (src/osqp_solver.py:6-155); QP solved exactly."""
 
     def __init__(self, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
-                 qp="exact", P=None):
+                 qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30):
         self.P_ = P or rbd.params()
         self.N, self.dt = N, dt
         self.nq = self.nv = rbd.NJ
@@ -61,6 +61,9 @@ class OSQPSolverRef:
         self.Pdata = np.zeros(self.P.nnz)
         self.Adata = np.zeros(self.A.nnz)
         self.qp = qp
+        # config 4 box mode (oracle/box_ipm.py)
+        self.box_mask, self.box_tol, self.box_max_iters = box_mask, box_tol, box_max_iters
+        self.last_ipm = None
         nq = self.nq
         self.A_k = np.vstack([-1.0 * np.eye(self.nx),
                               np.vstack([np.hstack([np.eye(nq), self.dt * np.eye(nq)]), np.ones((nq, 2 * nq))])])
@@ -198,7 +201,20 @@ class OSQPSolverRef:
         self.update_cost_matrix(xu, eepos_g)
         if self.qp == "admm":
             return self.solve_qp_admm()
+        if self.qp == "box":
+            return self.solve_qp_box()
         return self.solve_qp_exact()
+
+    def solve_qp_box(self):
+        """Config 4: box rows on q, v, u (oracle/box_ipm.py), from the equality-only optimum."""
+        from . import box_ipm
+        x_eq = self.solve_qp_exact().x
+        P, A = self.matrices()
+        Pf = (P + P.T - diags(P.diagonal())).tocsc()
+        lo, hi, bm = box_ipm.box_bounds(self.P_, self.N, self.box_mask)
+        r = box_ipm.ipm_box(Pf, self.g, A, self.l, x_eq, lo, hi, bm, tol=self.box_tol, max_iters=self.box_max_iters)
+        self.last_ipm = r
+        return QPResult(r.x, None, r.iters)
 
     # src/osqp_solver.py:146-155
     def eepos(self, q):

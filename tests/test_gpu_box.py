@@ -1,0 +1,103 @@
+"""Config 4 on the GPU: the box-constrained QP mode (I7M_QP_BOX) against its oracle
+(oracle/box_ipm.py, which the GPU path restates step by step), through the C-ABI.
+
+Tolerances (fp64):
+  QP minimiser vs oracle interior point      : 1e-6 relative (same iteration, same count;
+      both Newton solves are exact, the GPU's by Riccati, the oracle's by sparse LU, so only
+      rounding differs, amplified by Sigma ~ z/s near active bounds)
+  interior-point iteration counts            : identical
+  full SQP with box rows                     : 1e-5 relative, alpha sequence identical
+  config 4 at full size (B=4096, N=64)       : bounds hold exactly, >= 99% converged
+"""
+import numpy as np
+import pytest
+
+from oracle import box_ipm
+from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def _box_handle(lib, model, N, B, **kw):
+    return lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_BOX, **kw)
+
+
+def _relerr(a, b):
+    return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+def _qp_inputs(N, B, seed=46):
+    """Linearisation points that make box rows bind: the synthetic start (XU = 0 except x0)
+    and a quarter step towards the equality-only QP minimiser."""
+    xcur, goals, XU = synthetic_batch(B, N, seed)
+    s = OSQPSolverRef(N=N)
+    XU2 = XU.copy()
+    for b in range(B):
+        XU2[b] += 0.25 * (s.setup_and_solve_qp(XU[b], xcur[b], goals[b]).x - XU[b])
+    return np.vstack([xcur, xcur]), np.vstack([goals, goals]), np.vstack([XU, XU2])
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_box_qp_matches_oracle(lib, model, N):
+    xcur, goals, XU = _qp_inputs(N, 3)
+    B = XU.shape[0]
+    h = _box_handle(lib, model, N, B)
+    sol = h.qp(XU, xcur, goals)
+    it, conv, mu = h.box_stats(B)
+    ref = OSQPSolverRef(N=N, qp="box")
+    lo, hi, bm = box_ipm.box_bounds(ref.P_, N)
+    active = 0
+    for b in range(B):
+        x = ref.setup_and_solve_qp(XU[b], xcur[b], goals[b]).x
+        r = ref.last_ipm
+        assert conv[b] == r.converged and it[b] == r.iters, (b, it[b], r.iters)
+        assert _relerr(sol[b], x) <= 1e-6, (b, _relerr(sol[b], x))
+        assert (sol[b][bm] > lo[bm]).all() and (sol[b][bm] < hi[bm]).all()
+        active += int(((x - lo)[bm] < 1e-3).sum() + ((hi - x)[bm] < 1e-3).sum())
+    assert active > 0
+
+
+def test_box_sqp_matches_oracle(lib, model):
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, 46)
+    h = _box_handle(lib, model, N, B)
+    out, st = h.solve(xcur, goals, XU)
+    s = OSQPSolverRef(N=N, qp="box")
+    for b in range(B):
+        sq = SQPRef(s)
+        ref = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        al = list(st["alphas"][b][: st["n_alphas"][b]])
+        assert al == sq.stats["linesearch_alphas"]["values"], (b, al, sq.stats["linesearch_alphas"]["values"])
+        assert _relerr(out[b], ref) <= 1e-5, (b, _relerr(out[b], ref))
+
+
+def test_box_mask_zero_is_direct_mode(lib, model):
+    N, B = 32, 8
+    xcur, goals, XU = synthetic_batch(B, N, 47)
+    d = lib.Handle(model, N=N, max_batch=B).solve(xcur, goals, XU)[0]
+    b = _box_handle(lib, model, N, B, box_mask=0).solve(xcur, goals, XU)[0]
+    np.testing.assert_array_equal(d, b)
+
+
+def test_config4_full_size(lib, model):
+    """Config 4: B = 4096, N = 64, box rows on q, v, u."""
+    N, B = 64, 4096
+    from indy7_mpc_amd.synthetic import make_batch
+    h = _box_handle(lib, model, N, B)
+    xcur, goals, XU = make_batch(h, model, B, N, seed=46)
+    out, st = h.solve(xcur, goals, XU)
+    it, conv, mu = h.box_stats(B)
+    lo, hi, bm = box_ipm.box_bounds(OSQPSolverRef(N=N).P_, N)
+    assert np.isfinite(out).all()
+    assert (out[:, bm] >= lo[bm]).all() and (out[:, bm] <= hi[bm]).all()
+    assert conv.mean() >= 0.99, conv.mean()
+    np.testing.assert_array_equal(out[:, :12], xcur)
