@@ -62,6 +62,15 @@ def cpu_baseline(N: int, budget_s: float, seed: int, threads: int):
     cpu.solve(xm, gm, Xm, N, nthreads=threads)
     t3 = time.perf_counter()
     fl = [cpu.count_flops(xcur[b], goals[b], XU[b], N) for b in range(min(n, 64))]
+    # the numpy/scipy restatement (oracle/osqp_ref.py: the reference's per-knot Python structure,
+    # exact sparse-LU KKT instead of OSQP) on one core: the stand-in for osqp_sqp.py itself
+    from oracle.osqp_ref import OSQPSolverRef, SQPRef
+    sq = SQPRef(OSQPSolverRef(N=N))
+    npy_n, t4 = 0, time.perf_counter()
+    while npy_n < 4096 and (npy_n < 2 or time.perf_counter() - t4 < budget_s / 4):
+        sq.sqp(xcur[npy_n % n], goals[npy_n % n], XU[npy_n % n].copy())
+        npy_n += 1
+    t5 = time.perf_counter()
     per_iter_lin = fl[0]["linearize"] / fl[0]["iters"]
     per_iter_qp = fl[0]["qp"] / fl[0]["iters"]
     return {
@@ -69,6 +78,8 @@ def cpu_baseline(N: int, budget_s: float, seed: int, threads: int):
         "sample": f"{n} solves (config-3 draws, N={N}, seed {seed}) by oracle/cpp/i7m_cpu.cpp, 1 thread, "
                   f"{t1 - t0:.1f}s",
         "all_cores": {"value": nm / (t3 - t2), "cores": threads, "sample": f"{nm} solves, {threads} OpenMP threads"},
+        "numpy_restatement": {"value": npy_n / (t5 - t4), "cores": 1,
+                              "sample": f"{npy_n} solves by oracle/osqp_ref.py (numpy + scipy splu), {t5 - t4:.1f}s"},
         "cpu_model": _cpu_model(),
         "flops": {"per_solve_mean": float(np.mean([f["total"] for f in fl])),
                   "linearize_per_iter": per_iter_lin, "riccati_per_iter": per_iter_qp,
@@ -229,6 +240,15 @@ def main():
         if i >= 3:
             lat.append((time.perf_counter() - a) * 1e3)
 
+    # host-to-host rate (numpy in -> H2D + kernels + D2H -> numpy out, i7m_solve): the PCIe-
+    # inclusive figure of DESIGN.md §5, never `value`
+    h2h = []
+    for i in range(4):
+        a = time.perf_counter()
+        h.solve(xcur, goals, XU)
+        if i >= 1:
+            h2h.append(time.perf_counter() - a)
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -267,6 +287,7 @@ def main():
                    "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)"},
         "p50_latency_ms": statistics.median(step_ms),
         "p50_latency_b1_ms": statistics.median(lat),
+        "host_to_host_solves_per_s": B / statistics.median(h2h),
         "qp_iters_mean": qp_iters_mean,
         "kernels": per_kernel,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
