@@ -230,20 +230,25 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
   });
 }
 
+// base_from_lin: lin/cost of W hold the linearisation of this xu (the SQP loop), so the base
+// merit comes from them (k_linesearch); otherwise candidate 0 is evaluated.
 int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, double* xu,
                       const double* sol, const double* goals, int* active, ProblemStats* st, double* alpha_out,
-                      int iter, int mode) {
+                      int iter, int mode, bool base_from_lin) {
   if (P.B == 0) return I7M_OK;
+  const size_t lds = ls_lds_bytes(P.T);
+  const double* ln = base_from_lin ? W.lin : nullptr;
+  const double* cs = base_from_lin ? W.cost : nullptr;
   return timed(h, s, I7M_K_LINESEARCH, [&] {
     if (h->ablate == 4)
-      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode, ln, cs);
     else if (h->spec)
-      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode, ln, cs);
     else
-      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), 0, s, h->d_model, P, xu, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode);
+      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+                         active, st, alpha_out, iter, mode, ln, cs);
   });
 }
 
@@ -339,7 +344,8 @@ int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double
       if ((rc = launch_linearize(h, ss[c], W, P, xu, g, act))) return rc;
       const double* qsol = nullptr;
       if ((rc = solve_qp(h, ss[c], W, P, xu, xs, act, h->d_sol + o * T, &qsol))) return rc;
-      if ((rc = launch_linesearch(h, ss[c], W, P, xu, qsol, g, act, d_st + o, nullptr, it, 0))) return rc;
+      if ((rc = launch_linesearch(h, ss[c], W, P, xu, qsol, g, act, d_st + o, nullptr, it, 0, h->ablate != 6)))
+        return rc;
     }
   }
   if (C > 1) {  // join
@@ -651,7 +657,8 @@ int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_sol, xu_full, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = launch_linesearch(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1))) return rc;
+  if ((rc = launch_linesearch(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1,
+                             false))) return rc;
   if ((rc = copy_out(h, alpha, h->d_out, (size_t)B))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;

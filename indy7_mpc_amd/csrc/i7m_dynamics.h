@@ -86,11 +86,19 @@ __device__ __forceinline__ void inertia_mul(const DevModel& M, int i, const T l[
   fn[2] = I[2] * w[0] + I[4] * w[1] + I[5] * w[2] + (h[0] * l[1] - h[1] * l[0]);
 }
 
+// LDS parking of RNEA link forces (NLDS > 0, T = double only): element (link i, component k)
+// of this lane at fs[(6 i + k) * 64] — lane-interleaved, so a wave's accesses hit 64 banks.
+template <class T> __device__ __forceinline__ void lds_put(double* p, const T& v);
+template <> __device__ __forceinline__ void lds_put<double>(double* p, const double& v) { *p = v; }
+template <> __device__ __forceinline__ void lds_put<dual>(double*, const dual&) {}
+
 // Recursive Newton-Euler, local frames. c/s = cos/sin(q). Writes tau.
 // fext6: optional local spatial force (lin, ang) on the last body (pinocchio f_ext[6]).
-template <class T>
+// NLDS: the forces of links 0..NLDS-1, which live from the forward to the end of the backward
+// sweep, are kept in LDS (fs) instead of registers.
+template <class T, int NLDS = 0>
 __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[6], const T qd[6], const T qdd[6],
-                                     bool grav, const double* fext6, T tau[6]) {
+                                     bool grav, const double* fext6, T tau[6], double* fs = nullptr) {
   T vl[3] = {zero<T>(), zero<T>(), zero<T>()};
   T vw[3] = {zero<T>(), zero<T>(), zero<T>()};
   T al[3], aw[3] = {zero<T>(), zero<T>(), zero<T>()};
@@ -140,16 +148,31 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
     cross3(vw, hl, t1);
     cross3(vw, hn, t2);
     cross3(vl, hl, t3);
-    f[i][0] = il[0] + t1[0]; f[i][1] = il[1] + t1[1]; f[i][2] = il[2] + t1[2];
-    f[i][3] = in_[0] + t2[0] + t3[0]; f[i][4] = in_[1] + t2[1] + t3[1]; f[i][5] = in_[2] + t2[2] + t3[2];
+    T fi[6];
+    fi[0] = il[0] + t1[0]; fi[1] = il[1] + t1[1]; fi[2] = il[2] + t1[2];
+    fi[3] = in_[0] + t2[0] + t3[0]; fi[4] = in_[1] + t2[1] + t3[1]; fi[5] = in_[2] + t2[2] + t3[2];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      if (i < NLDS) lds_put<T>(fs + (6 * i + k) * 64, fi[k]);
+      else f[i][k] = fi[k];
+    }
   }
-  if (fext6) {
+  if (fext6 && NLDS < 6) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) f[5][k] = f[5][k] - cst<T>(fext6[k]);
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     __builtin_amdgcn_sched_barrier(0);
+    if (i < NLDS) {
+      if (i == 5) {  // the tip: no child contribution; the external wrench acts here
+#pragma unroll
+        for (int k = 0; k < 6; ++k) f[5][k] = cst<T>(fs[(30 + k) * 64]) - cst<T>(fext6 ? fext6[k] : 0.0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) f[i][k] = cst<T>(fs[(6 * i + k) * 64]) + f[i][k];
+      }
+    }
     tau[i] = f[i][5];
     if (i > 0) {
       const double* R = M.Rp[i];
@@ -166,12 +189,22 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
       rp(R, x, Nn);
       T tt[3] = {cst<T>(t[0]), cst<T>(t[1]), cst<T>(t[2])};
       cross3(tt, F, tF);
-      f[i - 1][0] = f[i - 1][0] + F[0];
-      f[i - 1][1] = f[i - 1][1] + F[1];
-      f[i - 1][2] = f[i - 1][2] + F[2];
-      f[i - 1][3] = f[i - 1][3] + Nn[0] + tF[0];
-      f[i - 1][4] = f[i - 1][4] + Nn[1] + tF[1];
-      f[i - 1][5] = f[i - 1][5] + Nn[2] + tF[2];
+      if (i - 1 < NLDS) {
+        // parked link: its own force is added when the sweep reaches it
+        f[i - 1][0] = F[0];
+        f[i - 1][1] = F[1];
+        f[i - 1][2] = F[2];
+        f[i - 1][3] = Nn[0] + tF[0];
+        f[i - 1][4] = Nn[1] + tF[1];
+        f[i - 1][5] = Nn[2] + tF[2];
+      } else {
+        f[i - 1][0] = f[i - 1][0] + F[0];
+        f[i - 1][1] = f[i - 1][1] + F[1];
+        f[i - 1][2] = f[i - 1][2] + F[2];
+        f[i - 1][3] = f[i - 1][3] + Nn[0] + tF[0];
+        f[i - 1][4] = f[i - 1][4] + Nn[1] + tF[1];
+        f[i - 1][5] = f[i - 1][5] + Nn[2] + tF[2];
+      }
     }
   }
 }
@@ -304,11 +337,13 @@ __device__ __forceinline__ void chol6_solve(const double L[6][6], double b[6]) {
 }
 
 // a = ABA(q, v, tau[, fext]) = M^-1 (tau - RNEA(q, v, 0)); L returns chol(M).
+// NLDS / fs: see rnea (LDS parking of link forces).
+template <int NLDS = 0>
 __device__ __forceinline__ void forward_dynamics(const DevModel& Md, const double c[6], const double s[6],
                                                  const double v[6], const double tau[6], const double* fext6,
-                                                 double L[6][6], double a[6]) {
+                                                 double L[6][6], double a[6], double* fs = nullptr) {
   double z[6] = {0, 0, 0, 0, 0, 0}, b[6];
-  rnea<double>(Md, c, s, v, z, true, fext6, b);
+  rnea<double, NLDS>(Md, c, s, v, z, true, fext6, b, fs);
 #pragma unroll
   for (int i = 0; i < 6; ++i) a[i] = tau[i] - b[i];
   __builtin_amdgcn_sched_barrier(0);

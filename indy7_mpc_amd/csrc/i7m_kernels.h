@@ -97,14 +97,28 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // itself, src/osqp_sqp.py:52-55), 1..8 = alphas 1, 1/2, ..., 1/128.  R = max(1, 64/N)
 // candidates per round; the first accepted candidate in alpha order wins (identical to the
 // sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha.
+// With lin / cost (the k_linearize outputs at this XU) the base merit is assembled from them —
+// a = ABA(q, v, u) and |e| of every knot are already there — so no round evaluates candidate 0.
 // SPEC: Indy7 constants baked in (kIndy7Model, generated from the URDF) instead of read from Mg.
+// k_linesearch register budget: 2 waves/SIMD (<= 256 VGPRs) with the forces of
+// links 0..2 parked in LDS and XU / sol staged in LDS: 18.3 KB LDS per wave at N = 32, i.e. 8
+// waves per CU.  Measured 151 -> 132 us (1 wave/SIMD before); staging matters more than the
+// ~90 B/lane of spill the 2-wave target leaves.
+constexpr int LS_NLDS = 3;  // links whose RNEA forces k_linesearch parks in LDS
+constexpr bool LS_STAGE = true;  // stage XU / sol in LDS (else read them through the caches)
+// dynamic LDS of k_linesearch for trajectory length T
+inline size_t ls_lds_bytes(int T) {
+  const int park = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
+  return sizeof(double) * (size_t)((LS_STAGE ? 2 * T : 0) + park);
+}
 template <bool SPEC, int ABL = 0>
-__global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    double* __restrict__ xu, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
                                                    int* __restrict__ active,
                                                    ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
-                                                   int iter, int mode) {
+                                                   int iter, int mode, const double* __restrict__ lin = nullptr,
+                                                   const double* __restrict__ cost = nullptr) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
@@ -117,56 +131,27 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
   double* X = xu + (long)b * P.T;
   const double* S = sol + (long)b * P.T;
   // the problem's XU and QP minimiser, staged once in LDS for every round
-  __shared__ double sX[18 * MAXN], sS[18 * MAXN];
-  __shared__ double part[64][4];
+  // dynamic LDS (ls_lds_bytes): sX | sS (T each) | RNEA link-force parking (rnea NLDS), which
+  // also holds the non-power-of-2 reduction (a different phase of each round)
+  extern __shared__ double ls_dyn[];
+  const double* sX = LS_STAGE ? ls_dyn : X;
+  const double* sS = LS_STAGE ? ls_dyn + P.T : S;
+  double* fpark = ls_dyn + (LS_STAGE ? 2 * P.T : 0);
+  double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
   __shared__ double merit[9];
-  for (int e = l; e < P.T; e += 64) {
-    sX[e] = X[e];
-    sS[e] = S[e];
+  if (LS_STAGE) {
+    for (int e = l; e < P.T; e += 64) {
+      ls_dyn[e] = X[e];
+      ls_dyn[P.T + e] = S[e];
+    }
   }
   const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
   const bool pow2 = (N & (N - 1)) == 0;
   const double* goal = goals + (long)b * N * P.goal_stride + (long)(k < N ? k : 0) * P.goal_stride;
   const double* f6 = fext ? fext + 6L * b : nullptr;
   __syncthreads();
-  double base = 0.0;
-  int found = -1;
-  for (int c0 = 0; c0 < 1 + NALPHA && found < 0; c0 += R) {
-    const int cand = c0 + slot;
-    double o[4] = {0.0, 0.0, 0.0, 0.0};
-    if (slot < R && k < N && cand < 1 + NALPHA) {
-      // knot k (18 values; the last knot has no u) and the state of knot k+1 (12 values)
-      const bool last = (k == N - 1);
-      const double al = (cand == 0) ? 0.0 : alphas[cand - 1];
-      const int ok = 18 * k, on = 18 * (last ? k : k + 1);
-      double x[18], xn[12];
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        const int ii = (last && i >= 12) ? 0 : i;
-        const double xv = sX[ok + ii];
-        x[i] = (cand == 0) ? xv : xv + al * (sS[ok + ii] - xv);
-      }
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const double xv = sX[on + i];
-        xn[i] = (cand == 0) ? xv : xv + al * (sS[on + i] - xv);
-      }
-      if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
-        o[0] = x[0] * x[1]; o[1] = x[6] * x[6]; o[2] = x[12] * xn[0]; o[3] = xn[6] + x[17];
-      } else {
-        merit_knot(Md, P, k, x, xn, goal, f6, o);
-      }
-      if (k == 0 && cand > 0) {
-        // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
-        double dd = 0.0;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          const double t = x[i] - sX[i];
-          dd += t * t;
-        }
-        o[3] += sqrt(dd);
-      }
-    }
+  // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
+  auto reduce_store = [&](double o[4], int c0) {
     if (pow2) {
       // tree-sum the N knots of each candidate slot with shuffles (segments of width N)
 #pragma unroll
@@ -188,6 +173,111 @@ __global__ void __launch_bounds__(64) k_linesearch(const DevModel* __restrict__ 
       }
     }
     __syncthreads();
+  };
+  int cstart = 0;
+  if (lin) {
+    // base merit (src/osqp_sqp.py:52-55) from the linearisation of this XU: |e| (cost[9]) and
+    // a = ABA(q, v, u) (lin[108..113]) per knot; slot 0 of the candidate layout
+    const double* LB = lin + (long)b * (N - 1) * LIN_STRIDE;
+    const double* CB = cost + (long)b * N * COST_STRIDE;
+    double o[4] = {0.0, 0.0, 0.0, 0.0};
+    if (slot == 0 && k < N) {
+      const bool last = (k == N - 1);
+      const int ok = 18 * k, on = 18 * (last ? k : k + 1);
+      const double nrm = CB[k * COST_STRIDE + 9];
+      o[0] = CB[k * COST_STRIDE + 6] * (nrm * nrm);
+      double vv = 0.0, uu = 0.0, eq = 0.0, ev = 0.0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) vv += sX[ok + 6 + i] * sX[ok + 6 + i];
+      o[1] = P.dQ * vv;
+      if (!last) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          uu += sX[ok + 12 + i] * sX[ok + 12 + i];
+          const double dq = (sX[ok + i] + sX[ok + 6 + i] * P.dt) - sX[on + i];
+          const double dv = (sX[ok + 6 + i] + LB[k * LIN_STRIDE + 108 + i] * P.dt) - sX[on + 6 + i];
+          eq += dq * dq;
+          ev += dv * dv;
+        }
+        o[2] = P.R * uu;
+        o[3] = sqrt(eq) + sqrt(ev);
+      }
+    }
+    reduce_store(o, 0);
+    cstart = 1;
+  }
+  double base = 0.0;
+  int found = -1;
+  for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R) {
+    const int cand = c0 + slot;
+    double o[4] = {0.0, 0.0, 0.0, 0.0};
+    if (slot < R && k < N && cand < 1 + NALPHA) {
+      // merit terms of (candidate, knot k): the knot values are recomputed from the LDS copy of
+      // XU / sol where they are used instead of being held in registers across the dynamics
+      // (the line-search point XU + al (sol - XU), src/osqp_sqp.py:60)
+      const bool last = (k == N - 1);
+      const bool base_pt = (cand == 0);
+      const double al = base_pt ? 0.0 : alphas[cand - 1];
+      const int ok = 18 * k, on = 18 * (last ? k : k + 1);
+      auto val = [&](int e) -> double {
+        const double xv = sX[e];
+        return base_pt ? xv : xv + al * (sS[e] - xv);
+      };
+      if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
+        o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
+        o[3] = val(on + 6) + val(ok + 11);
+      } else {
+        double c[6], sn[6], pe[3];
+        {
+          double q[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) q[i] = val(ok + i);
+          sincos6(q, c, sn);
+        }
+        fk_jac(Md, c, sn, pe, nullptr);
+        const double e0 = pe[0] - goal[0], e1 = pe[1] - goal[1], e2 = pe[2] - goal[2];
+        o[0] = (last ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
+        double vv = 0.0, uu = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double vi = val(ok + 6 + i);
+          vv += vi * vi;
+        }
+        o[1] = P.dQ * vv;
+        if (!last) {
+          double v[6], u[6], L[6][6], a[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            v[i] = val(ok + 6 + i);
+            u[i] = val(ok + 12 + i);
+            uu += u[i] * u[i];
+          }
+          o[2] = P.R * uu;
+          forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark + l);
+          asm volatile("" ::: "memory");  // re-read the knot values from LDS below
+          double eq = 0.0, ev = 0.0;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const double dq = (val(ok + i) + val(ok + 6 + i) * P.dt) - val(on + i);
+            const double dv = (val(ok + 6 + i) + a[i] * P.dt) - val(on + 6 + i);
+            eq += dq * dq;
+            ev += dv * dv;
+          }
+          o[3] = sqrt(eq) + sqrt(ev);
+        }
+      }
+      if (k == 0 && cand > 0) {
+        // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
+        double dd = 0.0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          const double t = val(i) - sX[i];
+          dd += t * t;
+        }
+        o[3] += sqrt(dd);
+      }
+    }
+    reduce_store(o, c0);
     base = merit[0];
     for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R && cc < 1 + NALPHA; ++cc) {
       if (merit[cc] <= base) { found = cc; break; }
