@@ -82,23 +82,24 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
   __shared__ double st0[KPW][6];
 
   const double* X = xu + (long)(valid ? b : 0) * P.T + 18 * (valid ? k : 0);
-  double q[6], v[6];
+  double v[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    q[i] = X[i];
-    v[i] = (dyn ? X[6 + i] : 0.0);
-  }
+  for (int i = 0; i < 6; ++i) v[i] = (dyn ? X[6 + i] : 0.0);
+  // each link-lane evaluates sincos of its own joint only; the knot's six lanes share them
   double c[6], s[6];
-  sincos6(q, c, s);
-
-  // ---- cost linearisation (lane 0 of each knot)
-  if (valid && j == 0) {
-    const double* goal = goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride;
-    cost_knot(Md, P, X, goal, k, cost + ((long)b * P.N + k) * COST_STRIDE);
+  {
+    double sj, cj;
+    sincos(X[j], &sj, &cj);
+    const int base = 6 * gg;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      c[i] = __shfl(cj, base + i, 64);
+      s[i] = __shfl(sj, base + i, 64);
+    }
   }
 
   // ---- 1. serial chain (every lane): world placement of each joint, S, V, A0 (qdd = 0)
-  double Rj[9], pj[3], Sj[6], Vj[6], A0j[6];
+  double Rj[9], pj[3], Sj[6], Vj[6], A0j[6], pE[3];
   {
     double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     double p[3] = {0, 0, 0};
@@ -142,6 +143,30 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
         for (int r = 0; r < 6; ++r) { Sj[r] = S[r]; Vj[r] = V[r]; A0j[r] = A[r]; }
       }
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) pE[r] = p[r];  // joint-6 origin = the end effector
+  }
+
+  // ---- cost linearisation (src/osqp_solver.py:103-135) from the chain: e = p_E - goal;
+  // LOCAL_WORLD_ALIGNED column J_j = z_j x (p_E - p_j) = z_j x p_E + (p_j x z_j), so lane j
+  // writes (J^T e)_j; lane 0 the weights.
+  if (valid) {
+    const double* goal = goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride;
+    const double e0 = pE[0] - goal[0], e1 = pE[1] - goal[1], e2 = pE[2] - goal[2];
+    const double* z = Sj + 3;
+    const double J0 = (z[1] * pE[2] - z[2] * pE[1]) + Sj[0];
+    const double J1 = (z[2] * pE[0] - z[0] * pE[2]) + Sj[1];
+    const double J2 = (z[0] * pE[1] - z[1] * pE[0]) + Sj[2];
+    double* co = cost + ((long)b * P.N + k) * COST_STRIDE;
+    co[j] = e0 * J0 + e1 * J1 + e2 * J2;
+    if (j == 0) {
+      const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      const double w = P.regularize ? (1.0 / (fabs(nrm) + P.eps)) : 1.0;
+      co[6] = (k == P.N - 1) ? P.QN : 1.0;
+      co[7] = P.dQ * w;
+      co[8] = P.R * w;
+      co[9] = nrm;
     }
   }
 
