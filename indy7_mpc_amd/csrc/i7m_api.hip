@@ -58,6 +58,7 @@ struct i7m_handle {
   // batch buffers (max_batch problems)
   double *d_xu = nullptr, *d_xs = nullptr, *d_goal = nullptr, *d_sol = nullptr, *d_lin = nullptr,
          *d_cost = nullptr, *d_kbuf = nullptr, *d_aux = nullptr, *d_out = nullptr;
+  double* d_qpd = nullptr;  // (max_batch, N-1, QPD_STRIDE) per-knot QP records (k_linearize -> k_riccati_mfma)
   int* d_active = nullptr;
   ProblemStats* d_stats = nullptr;
   double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
@@ -173,6 +174,7 @@ int timed(i7m_handle* h, hipStream_t s, int kid, F&& launch) {
 struct Bufs {
   double* lin;
   double* cost;
+  double* qpd;
   double* kbuf;
   const double* fext;  // nullptr: no external wrench
   // box mode only (nullptr otherwise)
@@ -184,7 +186,7 @@ struct Bufs {
 Bufs bufs_at(const i7m_handle* h, long b0) {
   const long N = h->cfg.N, T = 18 * N - 6;
   Bufs W{h->d_lin + b0 * (N - 1) * LIN_STRIDE, h->d_cost + b0 * N * COST_STRIDE,
-         h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr,
+         h->d_qpd + b0 * (N - 1) * QPD_STRIDE, h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr,
          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (h->cfg.qp_mode == I7M_QP_BOX) {
     W.bx = h->d_bx + b0 * T;
@@ -207,10 +209,10 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
   return timed(h, s, I7M_K_LIN, [&] {
     if (h->spec)
       hipLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost);
+                         W.lin, W.cost, W.qpd);
     else
       hipLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost);
+                         W.lin, W.cost, W.qpd);
   });
 }
 
@@ -222,11 +224,14 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
                          W.kbuf, sol);
     else if (h->ablate == 1)
-      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol);
     else if (h->ablate == 2)
-      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol);
     else
-      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, active, W.kbuf, sol);
+      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol);
   });
 }
 
@@ -281,8 +286,8 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   for (int it = 0; it < BP.max_iters; ++it) {
     for (int half = 0; half < 2; ++half) {
       rc = timed(h, s, I7M_K_RICCATI_BOX, [&] {
-        hipLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, P, xu, xs, W.lin, W.cost, W.bact, W.kbuf, sol,
-                           W.bsig, W.bh);
+        hipLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, P, xu, xs, W.lin, W.cost, W.qpd, W.bact, W.kbuf,
+                           sol, W.bsig, W.bh);
       });
       if (rc) return rc;
       rc = timed(h, s, I7M_K_IPM, [&] {
@@ -462,6 +467,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_sol, scratch * 8) && alloc((void**)&h->d_lin, Bm * (N - 1) * LIN_STRIDE * 8) &&
             alloc((void**)&h->d_cost, Bm * N * COST_STRIDE * 8) &&
             alloc((void**)&h->d_kbuf, Bm * (N - 1) * KBUF_STRIDE * 8) && alloc((void**)&h->d_aux, scratch * 8) &&
+            alloc((void**)&h->d_qpd, Bm * (N - 1) * QPD_STRIDE * 8) &&
             alloc((void**)&h->d_out, scratch * 8) &&
             alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
             alloc((void**)&h->d_fext, Bm * 6 * 8) && alloc((void**)&h->d_ric_desc, RIC_DESC_WORDS * 4);
@@ -490,7 +496,7 @@ void i7m_destroy(i7m_handle* h) {
   hipSetDevice(h->dev);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc,
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc, h->d_qpd,
                   h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact};
   for (void* p : bufs)
     if (p) hipFree(p);

@@ -20,6 +20,14 @@ namespace i7m {
 constexpr int LIN_STRIDE = 114;   // Aq(36) Av(36) Bu(36) a(6)
 constexpr int COST_STRIDE = 10;   // j(6) Qm dQm Rm |e|
 constexpr int KBUF_STRIDE = 84;   // K(6x12) kff(6) c_v(6)
+// per-knot QP record written by k_linearize for k_riccati_mfma (knots 0..N-2)
+constexpr int QPD_STRIDE = 32;
+constexpr int QPD_CV = 0;    // c_v (6): dynamics offset of the v rows
+constexpr int QPD_LX = 6;    // linear state terms (12): Qm j | dQm v
+constexpr int QPD_LU = 18;   // linear control terms (6): Rm u
+constexpr int QPD_J = 24;    // j = J^T e (6): the rank-1 factor of the q block
+constexpr int QPD_DQM = 30;  // dQm
+constexpr int QPD_RM = 31;   // Rm
 constexpr int NALPHA = 8;
 constexpr int MAXN = 64;
 

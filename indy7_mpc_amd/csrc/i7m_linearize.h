@@ -65,7 +65,8 @@ template <bool SPEC>
 __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
                                                   const double* __restrict__ xu, const double* __restrict__ goals,
                                                   const double* __restrict__ fext, const int* __restrict__ active,
-                                                  double* __restrict__ lin, double* __restrict__ cost) {
+                                                  double* __restrict__ lin, double* __restrict__ cost,
+                                                  double* __restrict__ qpd = nullptr) {
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   const int l = threadIdx.x;
   const int g = l / 6;
@@ -148,6 +149,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
     for (int r = 0; r < 3; ++r) pE[r] = p[r];  // joint-6 origin = the end effector
   }
 
+  double jte = 0.0, wreg = 1.0;  // (J^T e)_j and the cost regularisation weight of this knot
   // ---- cost linearisation (src/osqp_solver.py:103-135) from the chain: e = p_E - goal;
   // LOCAL_WORLD_ALIGNED column J_j = z_j x (p_E - p_j) = z_j x p_E + (p_j x z_j), so lane j
   // writes (J^T e)_j; lane 0 the weights.
@@ -159,13 +161,14 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
     const double J1 = (z[2] * pE[0] - z[0] * pE[2]) + Sj[1];
     const double J2 = (z[0] * pE[1] - z[1] * pE[0]) + Sj[2];
     double* co = cost + ((long)b * P.N + k) * COST_STRIDE;
-    co[j] = e0 * J0 + e1 * J1 + e2 * J2;
+    jte = e0 * J0 + e1 * J1 + e2 * J2;
+    co[j] = jte;
+    const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+    wreg = P.regularize ? (1.0 / (fabs(nrm) + P.eps)) : 1.0;
     if (j == 0) {
-      const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
-      const double w = P.regularize ? (1.0 / (fabs(nrm) + P.eps)) : 1.0;
       co[6] = (k == P.N - 1) ? P.QN : 1.0;
-      co[7] = P.dQ * w;
-      co[8] = P.R * w;
+      co[7] = P.dQ * wreg;
+      co[8] = P.R * wreg;
       co[9] = nrm;
     }
   }
@@ -390,6 +393,39 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
       }
     }
     out[108 + j] = acc[j];
+  }
+  if (qpd) {
+    // the knot's QP record for k_riccati_mfma (QPD_* layout): c_v = v + dt a - (Aq q + Av v + Bu u)
+    // (src/osqp_solver.py:76-81), the linear cost terms Qm j | dQm v | Rm u (src/osqp_solver.py:
+    // 121-135), j, dQm, Rm.  Row r of Aq/Av/Bu is spread over the knot's lanes (lane j owns
+    // column j): partial products go through the free tail of the LDS slot.
+    const double dt = P.dt;
+    const double qj = X[j], uj = dyn ? X[12 + j] : 0.0;
+    if (g < KPW) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const double aq = -dt * dq[r], av = (r == j ? 1.0 : 0.0) - dt * dv[r], bu = dt * em[r];
+        my[24 + r] = aq * qj + av * v[j] + bu * uj;
+      }
+    }
+    __syncthreads();
+    if (dyn) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) sacc += xs[gg][i][24 + j];
+      const double qm = (k == P.N - 1) ? P.QN : 1.0;
+      const double w = wreg;
+      double* o = qpd + ((long)b * (P.N - 1) + k) * QPD_STRIDE;
+      o[QPD_CV + j] = (v[j] + acc[j] * dt) - sacc;
+      o[QPD_LX + j] = qm * jte;
+      o[QPD_LX + 6 + j] = (P.dQ * w) * v[j];
+      o[QPD_LU + j] = (P.R * w) * uj;
+      o[QPD_J + j] = jte;
+      if (j == 0) {
+        o[QPD_DQM] = P.dQ * w;
+        o[QPD_RM] = P.R * w;
+      }
+    }
   }
 }
 

@@ -24,25 +24,25 @@ namespace i7m {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 enum : int {
-  MO_AQ = 0,     // stage stash: Aq(36) Av(36) Bu(36) a(6) | cost(10) | XU_k(18) | [BOX: Sigma(18) h(18)]
+  // stage stash: Aq(36) Av(36) Bu(36) | QP record of k_linearize (QPD_*, 32) | [BOX: Sigma(18) h(18)]
+  MO_AQ = 0,
   MO_AV = 36,
   MO_BU = 72,
-  MO_A = 108,
-  MO_W = 114,    // j(6) Qm dQm Rm |e|
-  MO_X = 124,
-  MO_SIG = 142,  // BOX: interior-point diagonal Sigma of the knot (q v u)
-  MO_HB = 160,   // BOX: linear-term shift h of the knot (q v u)
-  MO_CV = 178,   // 6
-  MO_RU = 184,   // 6   Rm u (+ h_u)
-  MO_QV = 190,   // 12  Qm j | dQm v
-  MO_LIN = 202,  // 12  BOX: linear state terms QV + h_x
-  MO_RD = 214,   // 6   BOX: R diagonal Rm + Sigma_u
-  MO_H = 220,    // 36
-  MO_G = 256,    // 78  G~ (6 x 13)
-  MO_KT = 334,   // 78  K~ (6 x 13)
-  MO_ZERO = 412,
-  MO_ONE = 413,
-  MO_TOTAL = 414,
+  MO_QP = 108,
+  MO_CV = MO_QP + QPD_CV,   // c_v (6)
+  MO_LX = MO_QP + QPD_LX,   // Qm j | dQm v (12)
+  MO_LU = MO_QP + QPD_LU,   // Rm u (6)
+  MO_J = MO_QP + QPD_J,     // j (6)
+  MO_DQM = MO_QP + QPD_DQM,
+  MO_RM = MO_QP + QPD_RM,
+  MO_SIG = 140,  // BOX: interior-point diagonal Sigma of the knot (q v u)
+  MO_HB = 158,   // BOX: linear-term shift h of the knot (q v u)
+  MO_H = 176,    // 36
+  MO_G = 212,    // 78  G~ (6 x 13)
+  MO_KT = 290,   // 78  K~ (6 x 13)
+  MO_ZERO = 368,
+  MO_ONE = 369,
+  MO_TOTAL = 370,
 };
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -75,7 +75,8 @@ __device__ __forceinline__ double rcp_nr(double d) {
 template <int ABL, bool BOX = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
                                                      const double* __restrict__ xs, const double* __restrict__ lin,
-                                                     const double* __restrict__ cost, const int* __restrict__ active,
+                                                     const double* __restrict__ cost, const double* __restrict__ qpd,
+                                                     const int* __restrict__ active,
                                                      double* __restrict__ kbuf, double* __restrict__ sol,
                                                      const double* __restrict__ bsig = nullptr,
                                                      const double* __restrict__ bh = nullptr) {
@@ -90,6 +91,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   const double* X = xu + (long)b * P.T;
   const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
   const double* CB = cost + (long)b * N * COST_STRIDE;
+  const double* QB = qpd + (long)b * (N - 1) * QPD_STRIDE;
   double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
 
   // ---- per-lane operand maps (fixed for the whole kernel)
@@ -117,22 +119,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     const int k = 4 * s + lq;
     offB[s - 1] = (k >= 6 && lr < 6) ? MO_BU + 6 * (k - 6) + lr : MO_ZERO;
   }
-  // Q~[lq+4i][lr] = sh[q1[i]] * sh[q2[i]];  R on the u diagonal;  N~ = r in column 12
-  // BOX: + Sigma on the state diagonal (oS), linear column from MO_LIN, R diagonal from MO_RD
-  constexpr int LINC = BOX ? MO_LIN : MO_QV;
-  int q1[4], q2[4], oR[4], oN[4], oS[4];
+  // Q~[lq+4i][lr] = sh[q1[i]] * sh[q2[i]]: rank-1 (Qm j) j' q block, dQm on the v diagonal, the
+  // linear terms in row / column 12;  R on the u diagonal;  N~ = r in column 12.
+  // BOX adds Sigma on the diagonals and h on the linear terms (oS for Q~, oR2 / oN2 for R, N~).
+  int q1[4], q2[4], oR[4], oN[4], oS[4], oR2[4], oN2[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = lq + 4 * i, c = lr;
     q1[i] = MO_ZERO;
     q2[i] = MO_ZERO;
-    if (r < 6 && c < 6) { q1[i] = MO_QV + r; q2[i] = MO_W + c; }
-    else if (r >= 6 && r < 12 && r == c) { q1[i] = MO_W + 7; q2[i] = MO_ONE; }
-    else if (r < 12 && c == 12) { q1[i] = LINC + r; q2[i] = MO_ONE; }
-    else if (r == 12 && c < 12) { q1[i] = LINC + c; q2[i] = MO_ONE; }
-    oR[i] = (r == c && r < 6) ? (BOX ? MO_RD + r : MO_W + 8) : MO_ZERO;
-    oN[i] = (c == 12 && r < 6) ? MO_RU + r : MO_ZERO;
-    oS[i] = (BOX && r == c && r < 12) ? MO_SIG + r : MO_ZERO;
+    if (r < 6 && c < 6) { q1[i] = MO_LX + r; q2[i] = MO_J + c; }
+    else if (r >= 6 && r < 12 && r == c) { q1[i] = MO_DQM; q2[i] = MO_ONE; }
+    else if (r < 12 && c == 12) { q1[i] = MO_LX + r; q2[i] = MO_ONE; }
+    else if (r == 12 && c < 12) { q1[i] = MO_LX + c; q2[i] = MO_ONE; }
+    oR[i] = (r == c && r < 6) ? MO_RM : MO_ZERO;
+    oN[i] = (c == 12 && r < 6) ? MO_LU + r : MO_ZERO;
+    oS[i] = MO_ZERO;
+    if (BOX) {
+      if (r == c && r < 12) oS[i] = MO_SIG + r;
+      else if (r < 12 && c == 12) oS[i] = MO_HB + r;
+      else if (r == 12 && c < 12) oS[i] = MO_HB + c;
+    }
+    oR2[i] = (BOX && r == c && r < 6) ? MO_SIG + 12 + r : MO_ZERO;
+    oN2[i] = (BOX && c == 12 && r < 6) ? MO_HB + 12 + r : MO_ZERO;
   }
   // K~[4s+lq][lr] for s = 0, 1
   int oK[2];
@@ -142,32 +151,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     oK[s] = (u < 6 && lr < 13) ? MO_KT + 13 * u + lr : MO_ZERO;
   }
 
-  // ---- terminal cost-to-go V~ = Q~_{N-1}
-  if (l < COST_STRIDE) sh[MO_W + l] = CB[(N - 1) * COST_STRIDE + l];
-  if (l < 12) sh[MO_X + l] = X[18 * (N - 1) + l];
-  if (BOX && l < 12) {
-    sh[MO_SIG + l] = bsig[(long)b * P.T + 18 * (N - 1) + l];
-    sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
-  }
-  if (l == 0) { sh[MO_ZERO] = 0.0; sh[MO_ONE] = 1.0; }
-  __syncthreads();
-  if (l < 12) {
-    const double qv = (l < 6) ? sh[MO_W + 6] * sh[MO_W + l] : sh[MO_W + 7] * sh[MO_X + l];
-    sh[MO_QV + l] = qv;
-    if (BOX) sh[MO_LIN + l] = qv + sh[MO_HB + l];
+  // ---- terminal cost-to-go V~ = Q~_{N-1}: the terminal knot's record from cost and XU
+  {
+    const double* ct = CB + (N - 1) * COST_STRIDE;
+    if (l < 6) {
+      sh[MO_J + l] = ct[l];
+      sh[MO_LX + l] = ct[6] * ct[l];
+    } else if (l < 12) {
+      sh[MO_LX + l] = ct[7] * X[18 * (N - 1) + l];
+    } else if (l == 12) {
+      sh[MO_DQM] = ct[7];
+    } else if (l == 13) {
+      sh[MO_ZERO] = 0.0;
+      sh[MO_ONE] = 1.0;
+    }
+    if (BOX && l < 12) {
+      sh[MO_SIG + l] = bsig[(long)b * P.T + 18 * (N - 1) + l];
+      sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
+    }
   }
   __syncthreads();
   d4 V;
 #pragma unroll
   for (int i = 0; i < 4; ++i) V[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
 
-  constexpr int SE = BOX ? 178 : 142;  // stash length
+  constexpr int SE = BOX ? 176 : 140;  // stash length
   auto src = [&](int k, int e) -> const double* {
-    if (e < LIN_STRIDE) return LINb + (long)k * LIN_STRIDE + e;
-    if (e < LIN_STRIDE + COST_STRIDE) return CB + k * COST_STRIDE + (e - LIN_STRIDE);
-    if (!BOX || e < 142) return X + 18 * k + (e - LIN_STRIDE - COST_STRIDE);
-    if (e < 160) return bsig + (long)b * P.T + 18 * k + (e - 142);
-    return bh + (long)b * P.T + 18 * k + (e - 160);
+    if (e < MO_QP) return LINb + (long)k * LIN_STRIDE + e;
+    if (e < MO_SIG) return QB + (long)k * QPD_STRIDE + (e - MO_QP);
+    if (e < MO_HB) return bsig + (long)b * P.T + 18 * k + (e - MO_SIG);
+    return bh + (long)b * P.T + 18 * k + (e - MO_HB);
   };
   const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
   double p0 = *src(N - 2, l), p1 = *src(N - 2, l + 64), p2 = *src(N - 2, e2);
@@ -179,23 +192,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
     __syncthreads();
     if (k > 0) { p0 = *src(k - 1, l); p1 = *src(k - 1, l + 64); p2 = *src(k - 1, e2); }
-    if (l < 6) {  // c_v = v + dt a - (Aq q + Av v + Bu u)   (src/osqp_solver.py:76-81)
-      double acc = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < 6; ++jj)
-        acc += sh[MO_AQ + 6 * l + jj] * sh[MO_X + jj] + sh[MO_AV + 6 * l + jj] * sh[MO_X + 6 + jj] +
-               sh[MO_BU + 6 * l + jj] * sh[MO_X + 12 + jj];
-      sh[MO_CV + l] = (sh[MO_X + 6 + l] + sh[MO_A + l] * dt) - acc;
-    } else if (l < 12) {
-      sh[MO_RU + l - 6] = sh[MO_W + 8] * sh[MO_X + 12 + (l - 6)] + (BOX ? sh[MO_HB + 12 + (l - 6)] : 0.0);
-      if (BOX) sh[MO_RD + l - 6] = sh[MO_W + 8] + sh[MO_SIG + 12 + (l - 6)];
-    } else if (l < 24) {
-      const int r = l - 12;
-      const double qv = (r < 6) ? sh[MO_W + 6] * sh[MO_W + r] : sh[MO_W + 7] * sh[MO_X + r];
-      sh[MO_QV + r] = qv;
-      if (BOX) sh[MO_LIN + r] = qv + sh[MO_HB + r];
-    }
-    __syncthreads();
     double bA[4], bB[2];
 #pragma unroll
     for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
@@ -205,8 +201,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       Qi[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
-      Ri[i] = sh[oR[i]];
-      Ni[i] = sh[oN[i]];
+      Ri[i] = sh[oR[i]] + (BOX ? sh[oR2[i]] : 0.0);
+      Ni[i] = sh[oN[i]] + (BOX ? sh[oN2[i]] : 0.0);
     }
     // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
     // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
