@@ -12,7 +12,9 @@ tail -2 $O/pytest_gpu.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
 cat $O/bench.json
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $R/tools/profile_kernels.py > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 3; }
+# the bench command itself under the kernel tracer (no CPU leg / config 4, to keep it short)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python $R/bench.py --no-cpu-baseline --no-config4 > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 3; }
+python $R/tools/trace_summary.py $O/trace/run_kernel_trace.csv --batch 4096 > $O/trace_summary.json
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o fetch -- python $R/tools/profile_kernels.py --steps 4 > $O/pmc_fetch.log 2>&1 || { tail -20 $O/pmc_fetch.log; exit 4; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o write -- python $R/tools/profile_kernels.py --steps 4 > $O/pmc_write.log 2>&1 || { tail -20 $O/pmc_write.log; exit 5; }
 ls -R $O | head -40

@@ -15,12 +15,17 @@ import os
 import statistics
 
 
+# kernel symbol -> the timing id bench.py reports (include/indy7_mpc.h I7M_K_*)
+CANON = {"k_riccati_mfma": "k_riccati"}
+
+
 def per_kernel(path, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r.get("Counter_Name") != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].split("::")[-1]
+        name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
+        name = CANON.get(name, name)
         grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
         vals[(name, grid)].append(float(r["Counter_Value"]))
     return vals
