@@ -5,6 +5,7 @@
 // sized once at i7m_create for max_batch problems (the reference's OSQP setup-once analogue,
 // src/osqp_solver.py:39-41).  No allocation or host sync inside i7m_solve_device.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -72,6 +73,16 @@ struct i7m_handle {
   bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
   size_t goal_cap = 0;
+  // hipGraph replay of run_sqp (run_sqp_graphed): a few instantiated graphs keyed by the call
+  struct GraphEntry {
+    int B, goal_stride, has_fext;
+    const void *xu, *xs, *goals, *st, *stream;
+    hipGraphExec_t exec;
+    unsigned long long last_use;
+  };
+  std::vector<GraphEntry> graphs;
+  unsigned long long graph_clock = 0;
+  bool use_graph = true;  // I7M_GRAPH=0 disables
   // concurrent problem ranges (run_sqp): worker streams + fork/join events
   int chunks = 0;  // 0: automatic (chunks_for), else I7M_CHUNKS
   hipStream_t workers[I7M_MAX_CHUNKS] = {};
@@ -152,20 +163,20 @@ hipEvent_t get_event(i7m_handle* h) {
   return e;
 }
 
+// Per-kernel timing: the start / stop events ride on the kernel's own dispatch packet
+// (hipExtLaunchKernelGGL), so timing adds no marker packets between launches; with timing off
+// the events are null and the launch is a plain dispatch.  `launch(ea, eb)` does the launch.
 template <class F>
 int timed(i7m_handle* h, hipStream_t s, int kid, F&& launch) {
   hipEvent_t a = nullptr, b = nullptr;
   if (h->timing) {
     a = get_event(h);
     b = get_event(h);
-    if (a && b) HIPCHK(hipEventRecord(a, s));
+    if (!a || !b) a = b = nullptr;
   }
-  launch();
+  launch(a, b);
   HIPCHK(hipGetLastError());
-  if (h->timing && a && b) {
-    HIPCHK(hipEventRecord(b, s));
-    h->ev.push_back({kid, a, b});
-  }
+  if (a && b) h->ev.push_back({kid, a, b});
   return I7M_OK;
 }
 
@@ -206,12 +217,12 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
   const long knots = (long)P.B * P.N;
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
-  return timed(h, s, I7M_K_LIN, [&] {
+  return timed(h, s, I7M_K_LIN, [&](hipEvent_t ea, hipEvent_t eb) {
     if (h->spec)
-      hipLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
+      hipExtLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
                          W.lin, W.cost, W.qpd);
     else
-      hipLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, h->d_model, P, xu, goals, W.fext, active,
+      hipExtLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
                          W.lin, W.cost, W.qpd);
   });
 }
@@ -219,19 +230,19 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
 int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
                    const double* xs, const int* active, double* sol) {
   if (P.B == 0) return I7M_OK;
-  return timed(h, s, I7M_K_RICCATI, [&] {
+  return timed(h, s, I7M_K_RICCATI, [&](hipEvent_t ea, hipEvent_t eb) {
     if (h->ric_impl == 1)
-      hipLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
+      hipExtLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
                          W.kbuf, sol);
     else if (h->ablate == 1)
-      hipLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol);
+      hipExtLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
     else if (h->ablate == 2)
-      hipLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol);
+      hipExtLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
     else
-      hipLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol);
+      hipExtLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
   });
 }
 
@@ -244,15 +255,15 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
   const size_t lds = ls_lds_bytes(P.T);
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
-  return timed(h, s, I7M_K_LINESEARCH, [&] {
+  return timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
     if (h->ablate == 4)
-      hipLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
     else if (h->spec)
-      hipLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
     else
-      hipLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
   });
 }
@@ -278,24 +289,24 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   if (h->cfg.qp_mode != I7M_QP_BOX || P.B == 0) return I7M_OK;
   const BoxParams BP = box_params(h);
   const dim3 g(P.B), blk(64);
-  rc = timed(h, s, I7M_K_IPM, [&] {
-    hipLaunchKernelGGL(k_ipm_init, g, blk, 0, s, h->d_model, P, BP, sol, active, W.bx, W.bzl, W.bzu, W.bsig, W.bh,
+  rc = timed(h, s, I7M_K_IPM, [&](hipEvent_t ea, hipEvent_t eb) {
+    hipExtLaunchKernelGGL(k_ipm_init, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, sol, active, W.bx, W.bzl, W.bzu, W.bsig, W.bh,
                        W.bst, W.bact);
   });
   if (rc) return rc;
   for (int it = 0; it < BP.max_iters; ++it) {
     for (int half = 0; half < 2; ++half) {
-      rc = timed(h, s, I7M_K_RICCATI_BOX, [&] {
-        hipLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, P, xu, xs, W.lin, W.cost, W.qpd, W.bact, W.kbuf,
+      rc = timed(h, s, I7M_K_RICCATI_BOX, [&](hipEvent_t ea, hipEvent_t eb) {
+        hipExtLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, W.bact, W.kbuf,
                            sol, W.bsig, W.bh);
       });
       if (rc) return rc;
-      rc = timed(h, s, I7M_K_IPM, [&] {
+      rc = timed(h, s, I7M_K_IPM, [&](hipEvent_t ea, hipEvent_t eb) {
         if (half == 0)
-          hipLaunchKernelGGL(k_ipm_pred, g, blk, 0, s, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bh,
+          hipExtLaunchKernelGGL(k_ipm_pred, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bh,
                              W.bst, W.bact);
         else
-          hipLaunchKernelGGL(k_ipm_corr, g, blk, 0, s, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bsig,
+          hipExtLaunchKernelGGL(k_ipm_corr, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, sol, W.bx, W.bzl, W.bzu, W.bdxa, W.bsig,
                              W.bh, W.bst, W.bact);
       });
       if (rc) return rc;
@@ -359,6 +370,53 @@ int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double
       HIPCHK(hipStreamWaitEvent(h->stream, h->join[c], 0));
     }
   }
+  return I7M_OK;
+}
+
+void drop_graphs(i7m_handle* h) {
+  for (auto& g : h->graphs) hipGraphExecDestroy(g.exec);
+  h->graphs.clear();
+}
+
+// run_sqp through a cached hipGraph: the 6-8 launches of a solve become one graph launch, which
+// removes the per-launch host cost and the dispatch gaps (what dominates small-batch latency).
+// A graph is keyed by every argument that reaches a kernel; a miss captures the same launch
+// sequence once.  Timing runs (events) and multi-range runs go direct.
+int run_sqp_graphed(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double* d_goals, int goal_stride,
+                    ProblemStats* d_st) {
+  if (!h->use_graph || h->timing || chunks_for(h, B) > 1) return run_sqp(h, B, d_xu, d_xs, d_goals, goal_stride, d_st);
+  const int hf = h->has_fext ? 1 : 0;
+  i7m_handle::GraphEntry* hit = nullptr;
+  for (auto& g : h->graphs)
+    if (g.B == B && g.goal_stride == goal_stride && g.has_fext == hf && g.xu == d_xu && g.xs == d_xs &&
+        g.goals == d_goals && g.st == d_st && g.stream == (const void*)h->stream)
+      hit = &g;
+  if (!hit) {
+    HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = run_sqp(h, B, d_xu, d_xs, d_goals, goal_stride, d_st);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->stream, &graph);
+    if (rc) {
+      if (graph) hipGraphDestroy(graph);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(I7M_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    if (ei != hipSuccess) return fail(I7M_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    if (h->graphs.size() >= 4) {  // evict the least recently used
+      size_t lru = 0;
+      for (size_t i = 1; i < h->graphs.size(); ++i)
+        if (h->graphs[i].last_use < h->graphs[lru].last_use) lru = i;
+      hipGraphExecDestroy(h->graphs[lru].exec);
+      h->graphs.erase(h->graphs.begin() + lru);
+    }
+    h->graphs.push_back({B, goal_stride, hf, d_xu, d_xs, d_goals, d_st, (const void*)h->stream, exec, 0});
+    hit = &h->graphs.back();
+  }
+  hit->last_use = ++h->graph_clock;
+  HIPCHK(hipGraphLaunch(hit->exec, h->stream));
   return I7M_OK;
 }
 
@@ -452,6 +510,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
   if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
   if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
+  if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c)
     if (hipStreamCreateWithFlags(&h->workers[c], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->join[c], hipEventDisableTiming) != hipSuccess)
@@ -505,6 +564,7 @@ void i7m_destroy(i7m_handle* h) {
     hipEventDestroy(t.b);
   }
   for (auto e : h->pool) hipEventDestroy(e);
+  drop_graphs(h);
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c) {
     if (h->workers[c]) {
       hipStreamSynchronize(h->workers[c]);
@@ -555,7 +615,7 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (d_xu_out != d_xu_in)
     HIPCHK(hipMemcpyAsync(d_xu_out, d_xu_in, (size_t)B * T * 8, hipMemcpyDeviceToDevice, h->stream));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
-  return run_sqp(h, B, d_xu_out, d_xcur, d_goals, goal_stride, st);
+  return run_sqp_graphed(h, B, d_xu_out, d_xcur, d_goals, goal_stride, st);
 }
 
 int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,
@@ -569,7 +629,7 @@ int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur,
   if ((rc = copy_in(h, h->d_xu, xu_in, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = run_sqp(h, B, h->d_xu, h->d_xs, h->d_goal, goal_stride, h->d_stats))) return rc;
+  if ((rc = run_sqp_graphed(h, B, h->d_xu, h->d_xs, h->d_goal, goal_stride, h->d_stats))) return rc;
   if ((rc = copy_out(h, xu_out, h->d_xu, (size_t)B * T))) return rc;
   if (stats)
     HIPCHK(hipMemcpyAsync(stats, h->d_stats, sizeof(ProblemStats) * (size_t)B, hipMemcpyDeviceToHost, h->stream));
