@@ -25,8 +25,8 @@ MAX_SQP = 8
 MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
-I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_COUNT = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm")
+I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_COUNT = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused")
 
 
 class I7MError(RuntimeError):

@@ -69,6 +69,7 @@ struct i7m_handle {
   int* d_bact = nullptr;
   uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
   int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
+  bool ipm_split = false;          // I7M_IPM=split: one launch per IPM phase instead of k_ipm_fused
   int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
   bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
@@ -289,6 +290,15 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   if (h->cfg.qp_mode != I7M_QP_BOX || P.B == 0) return I7M_OK;
   const BoxParams BP = box_params(h);
   const dim3 g(P.B), blk(64);
+  if (!h->ipm_split) {
+    rc = timed(h, s, I7M_K_IPM_FUSED, [&](hipEvent_t ea, hipEvent_t eb) {
+      hipExtLaunchKernelGGL(k_ipm_fused, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd, active,
+                            W.kbuf, (const double*)sol, sol, W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst, W.bact);
+    });
+    if (rc) return rc;
+    *out = W.bx;
+    return I7M_OK;
+  }
   rc = timed(h, s, I7M_K_IPM, [&](hipEvent_t ea, hipEvent_t eb) {
     hipExtLaunchKernelGGL(k_ipm_init, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, sol, active, W.bx, W.bzl, W.bzu, W.bsig, W.bh,
                        W.bst, W.bact);
@@ -509,6 +519,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   // developer knob for A/B profiling of the two QP kernels (default: MFMA)
   if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
   if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
+  if (const char* e = std::getenv("I7M_IPM")) h->ipm_split = std::strcmp(e, "split") == 0;
   if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c)

@@ -9,6 +9,7 @@
 #pragma once
 
 #include "i7m_kernels.h"
+#include "i7m_riccati_mfma.h"
 
 namespace i7m {
 
@@ -67,16 +68,17 @@ __device__ __forceinline__ double ratio_min(double t, double v, double dv) {
   return (dv < 0.0) ? fmin(t, -v / dv) : t;
 }
 
+// The three phases of one interior-point iteration, as wave-level device functions of problem
+// b (one wavefront; every lane ends with the same IpmState, reductions are xor-shuffle trees).
+// k_ipm_init / k_ipm_pred / k_ipm_corr launch them one at a time (I7M_IPM=split), and
+// k_ipm_fused runs the whole iteration of one problem in one wave.
+
 // x = clip(x_eq) into the interior, z = 1, mu, and the first predictor's Sigma and h.
-__global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
-                                                 const double* __restrict__ xeq, const int* __restrict__ active,
-                                                 double* __restrict__ x, double* __restrict__ zl, double* __restrict__ zu,
-                                                 double* __restrict__ sig, double* __restrict__ h,
-                                                 IpmState* __restrict__ st, int* __restrict__ ipm_active) {
-  const int b = blockIdx.x;
-  if (b >= P.B) return;
+__device__ __forceinline__ IpmState ipm_init_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+                                                  const double* __restrict__ xeq, double* __restrict__ x,
+                                                  double* __restrict__ zl, double* __restrict__ zu,
+                                                  double* __restrict__ sig, double* __restrict__ h) {
   const int l = threadIdx.x;
-  const DevModel& M = *Mg;
   const long o = (long)b * P.T;
   double acc = 0.0;
   int nb = 0;
@@ -99,30 +101,24 @@ __global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg
   }
   acc = wave_sum(acc);
   nb = wave_isum(nb);
-  if (l == 0) {
-    IpmState S;
-    S.mu = nb ? acc / (2.0 * nb) : 0.0;
-    S.rfrac = 1.0;
-    S.smu = 0.0;
-    S.iters = 0;
-    S.nb = nb;
-    S.converged = (nb == 0);
-    S.pad = 0;
-    st[b] = S;
-    ipm_active[b] = (active ? active[b] : 1) && nb > 0;
-  }
+  IpmState S;
+  S.mu = nb ? acc / (2.0 * nb) : 0.0;
+  S.rfrac = 1.0;
+  S.smu = 0.0;
+  S.iters = 0;
+  S.nb = nb;
+  S.converged = (nb == 0);
+  S.pad = 0;
+  return S;
 }
 
-// Predictor: dx_aff = y - x; affine step lengths and mu_aff; sigma*mu; the corrector's h.
-__global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
-                                                 const double* __restrict__ y, const double* __restrict__ x,
-                                                 const double* __restrict__ zl, const double* __restrict__ zu,
-                                                 double* __restrict__ dxa, double* __restrict__ h,
-                                                 IpmState* __restrict__ st, const int* __restrict__ ipm_active) {
-  const int b = blockIdx.x;
-  if (b >= P.B || !ipm_active[b]) return;
+// Predictor: dx_aff = y - x; affine step lengths and mu_aff; sigma*mu (-> S.smu); the
+// corrector's h.
+__device__ __forceinline__ void ipm_pred_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+                                              const double* __restrict__ y, const double* __restrict__ x,
+                                              const double* __restrict__ zl, const double* __restrict__ zu,
+                                              double* __restrict__ dxa, double* __restrict__ h, IpmState& S) {
   const int l = threadIdx.x;
-  const DevModel& M = *Mg;
   const long o = (long)b * P.T;
   double ap = 1.0, ad = 1.0;
   for (int e = l; e < P.T; e += 64) {
@@ -148,7 +144,6 @@ __global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg
     }
   }
   acc = wave_sum(acc);
-  IpmState S = st[b];
   const double mua = acc / (2.0 * S.nb);
   const double r = mua / S.mu;
   const double smu = r * r * r * S.mu;
@@ -163,23 +158,19 @@ __global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg
     }
     h[o + e] = hv;
   }
-  if (l == 0) st[b].smu = smu;
+  S.smu = smu;
 }
 
 // Corrector: dx = y - x, common step, update (x, z_l, z_u), new mu, convergence, and the next
 // predictor's Sigma and h.
-__global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
-                                                 const double* __restrict__ y, double* __restrict__ x,
-                                                 double* __restrict__ zl, double* __restrict__ zu,
-                                                 const double* __restrict__ dxa, double* __restrict__ sig,
-                                                 double* __restrict__ h, IpmState* __restrict__ st,
-                                                 int* __restrict__ ipm_active) {
-  const int b = blockIdx.x;
-  if (b >= P.B || !ipm_active[b]) return;
+__device__ __forceinline__ void ipm_corr_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+                                              const double* __restrict__ y, double* __restrict__ x,
+                                              double* __restrict__ zl, double* __restrict__ zu,
+                                              const double* __restrict__ dxa, double* __restrict__ sig,
+                                              double* __restrict__ h, IpmState& S) {
   const int l = threadIdx.x;
-  const DevModel& M = *Mg;
   const long o = (long)b * P.T;
-  const double smu = st[b].smu;
+  const double smu = S.smu;
   double t = 1.0;
   for (int e = l; e < P.T; e += 64) {
     double lo, hi;
@@ -221,14 +212,112 @@ __global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg
     }
   }
   acc = wave_sum(acc);
-  if (l == 0) {
-    IpmState S = st[b];
-    S.mu = acc / (2.0 * S.nb);
-    S.rfrac *= 1.0 - al;
-    S.iters += 1;
-    S.converged = (S.mu < BP.tol && S.rfrac < BP.tol);
+  S.mu = acc / (2.0 * S.nb);
+  S.rfrac *= 1.0 - al;
+  S.iters += 1;
+  S.converged = (S.mu < BP.tol && S.rfrac < BP.tol);
+}
+
+// The state is wave-uniform (every lane computed it from the same xor-shuffle reductions);
+// readfirstlane tells the compiler so, and the state lives in SGPRs across the Newton steps.
+__device__ __forceinline__ void ipm_uniform(IpmState& S) {
+  S.mu = readlane_f64(S.mu, 0);
+  S.rfrac = readlane_f64(S.rfrac, 0);
+  S.smu = readlane_f64(S.smu, 0);
+  S.iters = __builtin_amdgcn_readfirstlane(S.iters);
+  S.nb = __builtin_amdgcn_readfirstlane(S.nb);
+  S.converged = __builtin_amdgcn_readfirstlane(S.converged);
+}
+
+__device__ __forceinline__ bool ipm_done(const IpmState& S, const BoxParams& BP) {
+  return S.converged || S.iters >= BP.max_iters;
+}
+
+__global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ xeq, const int* __restrict__ active,
+                                                 double* __restrict__ x, double* __restrict__ zl, double* __restrict__ zu,
+                                                 double* __restrict__ sig, double* __restrict__ h,
+                                                 IpmState* __restrict__ st, int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  const IpmState S = ipm_init_body(*Mg, P, BP, b, xeq, x, zl, zu, sig, h);
+  if (threadIdx.x == 0) {
     st[b] = S;
-    if (S.converged || S.iters >= BP.max_iters) ipm_active[b] = 0;
+    ipm_active[b] = (active ? active[b] : 1) && S.nb > 0;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ y, const double* __restrict__ x,
+                                                 const double* __restrict__ zl, const double* __restrict__ zu,
+                                                 double* __restrict__ dxa, double* __restrict__ h,
+                                                 IpmState* __restrict__ st, const int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B || !ipm_active[b]) return;
+  IpmState S = st[b];
+  ipm_pred_body(*Mg, P, BP, b, y, x, zl, zu, dxa, h, S);
+  if (threadIdx.x == 0) st[b].smu = S.smu;
+}
+
+__global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP,
+                                                 const double* __restrict__ y, double* __restrict__ x,
+                                                 double* __restrict__ zl, double* __restrict__ zu,
+                                                 const double* __restrict__ dxa, double* __restrict__ sig,
+                                                 double* __restrict__ h, IpmState* __restrict__ st,
+                                                 int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B || !ipm_active[b]) return;
+  IpmState S = st[b];
+  ipm_corr_body(*Mg, P, BP, b, y, x, zl, zu, dxa, sig, h, S);
+  if (threadIdx.x == 0) {
+    st[b] = S;
+    if (ipm_done(S, BP)) ipm_active[b] = 0;
+  }
+}
+
+// The whole interior-point solve of one problem in one wavefront: init from the equality-QP
+// minimiser xeq, then predictor / corrector Newton steps (each a riccati_mfma_body<0, true> on
+// the problem's linearisation) until the problem converges or reaches max_iters.  One launch
+// per QP instead of 2 + 4 max_iters; each wave runs exactly its own iteration count and the
+// iteration state stays in registers.  Same arithmetic as the split kernels, phase for phase.
+// Newton iterates go to y (B, T), the iterate to x.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_ipm_fused(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP, const double* __restrict__ xu,
+            const double* __restrict__ xs, const double* __restrict__ lin, const double* __restrict__ cost,
+            const double* __restrict__ qpd, const int* __restrict__ active, double* __restrict__ kbuf,
+            const double* __restrict__ xeq, double* y, double* x, double* zl, double* zu, double* sig, double* h,
+            double* dxa, IpmState* __restrict__ st, int* __restrict__ ipm_active) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  __shared__ double sh[MO_TOTAL];
+  const DevModel& M = *Mg;
+  IpmState S = ipm_init_body(M, P, BP, b, xeq, x, zl, zu, sig, h);
+  ipm_uniform(S);
+  bool run = (active ? active[b] != 0 : true) && S.nb > 0;
+  // one Riccati call site (half 0: predictor, half 1: corrector) keeps one inlined copy
+  // The lane id and the model pointer are laundered per step (an empty asm the compiler must
+  // treat as redefining them), so the Riccati operand maps and the box bounds are rebuilt per
+  // step instead of hoisted out of the loop and held live across it (which spills).
+  for (int half = 0; run; half ^= 1) {
+    int l = threadIdx.x;
+    const DevModel* Mp = Mg;
+    asm volatile("" : "+v"(l));
+    asm volatile("" : "+s"(Mp));
+    __syncthreads();
+    riccati_mfma_body<0, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l);
+    __syncthreads();
+    if (half == 0) {
+      ipm_pred_body(*Mp, P, BP, b, y, x, zl, zu, dxa, h, S);
+      ipm_uniform(S);
+    } else {
+      ipm_corr_body(*Mp, P, BP, b, y, x, zl, zu, dxa, sig, h, S);
+      ipm_uniform(S);
+      run = !ipm_done(S, BP);
+    }
+  }
+  if (threadIdx.x == 0) {
+    st[b] = S;
+    ipm_active[b] = 0;
   }
 }
 

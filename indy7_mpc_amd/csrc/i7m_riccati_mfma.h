@@ -72,22 +72,18 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // x + dx itself.
 // 4 waves/SIMD (<= 128 VGPRs, MFMA accumulators in VGPRs): B = 4096 single-wave problems fit the
 // 1024 SIMDs in one round.
-template <int ABL, bool BOX = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
-                                                     const double* __restrict__ xs, const double* __restrict__ lin,
-                                                     const double* __restrict__ cost, const double* __restrict__ qpd,
-                                                     const int* __restrict__ active,
-                                                     double* __restrict__ kbuf, double* __restrict__ sol,
-                                                     const double* __restrict__ bsig = nullptr,
-                                                     const double* __restrict__ bh = nullptr) {
-  const int b = blockIdx.x;
-  if (b >= P.B) return;
-  if (active && !active[b]) return;
-  const int l = threadIdx.x;
+// The body of one problem's solve (problem b, one wavefront, lane l, `sh` = MO_TOTAL doubles of
+// LDS); k_riccati_mfma runs it once, k_ipm_fused (i7m_box.h) once per Newton step.
+template <int ABL, bool BOX>
+__device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
+                                                  const double* __restrict__ xs, const double* __restrict__ lin,
+                                                  const double* __restrict__ cost, const double* __restrict__ qpd,
+                                                  double* __restrict__ kbuf, double* __restrict__ sol,
+                                                  const double* __restrict__ bsig, const double* __restrict__ bh,
+                                                  double* __restrict__ sh, const int l) {
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
   const double dt = P.dt;
-  __shared__ double sh[MO_TOTAL];
   const double* X = xu + (long)b * P.T;
   const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
   const double* CB = cost + (long)b * N * COST_STRIDE;
@@ -358,6 +354,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     xreg = nx;
     if (l < 12) S[18 * (k + 1) + l] = nx;
   }
+}
+
+template <int ABL, bool BOX = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
+                                                     const double* __restrict__ xs, const double* __restrict__ lin,
+                                                     const double* __restrict__ cost, const double* __restrict__ qpd,
+                                                     const int* __restrict__ active,
+                                                     double* __restrict__ kbuf, double* __restrict__ sol,
+                                                     const double* __restrict__ bsig = nullptr,
+                                                     const double* __restrict__ bh = nullptr) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  __shared__ double sh[MO_TOTAL];
+  riccati_mfma_body<ABL, BOX>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, bsig, bh, sh, threadIdx.x);
 }
 
 }  // namespace i7m
