@@ -238,6 +238,9 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
     else if (h->ablate == 1)
       hipExtLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
                          sol, (const double*)nullptr, (const double*)nullptr);
+    else if (h->ablate == 8)
+      hipExtLaunchKernelGGL(k_riccati_mfma<4>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
     else if (h->ablate == 2)
       hipExtLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
                          sol, (const double*)nullptr, (const double*)nullptr);

@@ -42,7 +42,8 @@ enum : int {
   MO_KT = 290,   // 78  K~ (6 x 13)
   MO_ZERO = 368,
   MO_ONE = 369,
-  MO_TOTAL = 370,
+  MO_GJ = 370,   // 6 x 40  per-pivot Gauss-Jordan exchange slots
+  MO_TOTAL = 610,
 };
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -219,53 +220,95 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     Z11 = mfma(bB[1], W1[2], Z11);
     d4 Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
-    // H (6x6) and G~ (6x13) to LDS: rows lq + 4i < 6
+    double* kk = KB + (long)k * KBUF_STRIDE;
+    if (!(ABL & 4)) {
+      // K~ = -H^-1 G~ by Gauss-Jordan on [H | G~] (6 x 19) in place in the MFMA accumulator
+      // layout: lane l holds column lr of rows lq and lq + 4 (lq < 2) of H (lr < 6) and of G~
+      // (lr < 13).  Pivot p needs, per lane, M[r][p] of its two rows (published by the lanes
+      // lr == p) and M[p][lr] of its column (published by the lanes lq == p & 3): a per-pivot
+      // LDS slot, two writes and three broadcast-friendly reads, instead of 12 v_readlane per
+      // pivot.  The arithmetic is the column-per-lane elimination's, operation for operation.
+      // SPD H: no pivoting.  K~ ends where the V~ update wants it: the A operand of k-step s is
+      // K~[4s + lq][lr], i.e. this lane's G~ entry of row lq + 4s.
+      double eh0 = Z11[0], eh1 = Z11[1], eg0 = Z10[0], eg1 = Z10[1];
+      if (ABL & 2) {
+        eh0 *= 1e-3; eh1 *= 1e-3; eg0 *= 1e-3; eg1 *= 1e-3;
+      } else {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = lq + 4 * i;
-      if (r < 6) {
-        if (lr < 6) sh[MO_H + 6 * r + lr] = Z11[i];
-        if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
+        for (int p = 0; p < 6; ++p) {
+          double* col = sh + MO_GJ + 40 * p;  // col[2 lq + i] = M[lq + 4i][p]
+          double* row = col + 8;              // row[2 lr + j] = M[p][lr] of H (j = 0), G~ (j = 1)
+          if (lr == p) {
+            col[2 * lq] = eh0;
+            col[2 * lq + 1] = eh1;
+          }
+          if (lq == (p & 3)) {
+            row[2 * lr] = (p >> 2) ? eh1 : eh0;
+            row[2 * lr + 1] = (p >> 2) ? eg1 : eg0;
+          }
+          __syncthreads();
+          const double mr0 = col[2 * lq], mr1 = col[2 * lq + 1];
+          const double mph = row[2 * lr], mpg = row[2 * lr + 1];
+          const double inv = rcp_nr(row[2 * p]);
+          const double eph = mph * inv, epg = mpg * inv;
+          eh0 = (lq == p) ? eph : eh0 - mr0 * eph;
+          eg0 = (lq == p) ? epg : eg0 - mr0 * epg;
+          eh1 = (lq + 4 == p) ? eph : eh1 - mr1 * eph;
+          eg1 = (lq + 4 == p) ? epg : eg1 - mr1 * epg;
+        }
       }
-    }
-    __syncthreads();
-    // K~ = -H^-1 G~ by Gauss-Jordan on [H | G~] (6 x 19), one column per lane (lanes 0..18):
-    // the pivot column lives in lane p and is broadcast with v_readlane, so the factorisation is
-    // done once (not once per right-hand side) and needs no LDS round trip.  SPD H: no pivoting.
-    {
+      const double ka0 = (lr < 13) ? -eg0 : 0.0;
+      const double ka1 = (lq < 2 && lr < 13) ? -eg1 : 0.0;
+      // V~ <- Qxx + K~' G~
+      V = mfma(ka0, Z10[0], Z00);
+      V = mfma(ka1, Z10[1], V);
+      // K~ (78, row-major 6 x 13) and c_v (6) -> global for the forward rollout; stage 0 also
+      // stays in LDS (the rollout reads it from there)
+      if (lr < 13) {
+        kk[13 * lq + lr] = ka0;
+        if (lq < 2) kk[13 * (lq + 4) + lr] = ka1;
+        if (k == 0) {
+          sh[MO_KT + 13 * lq + lr] = ka0;
+          if (lq < 2) sh[MO_KT + 13 * (lq + 4) + lr] = ka1;
+        }
+      }
+      if (l < 6) kk[78 + l] = sh[MO_CV + l];
+    } else {
+      // (diagnostic A/B, I7M_ABLATE=8) column-per-lane Gauss-Jordan with v_readlane pivot
+      // broadcast: H, G~ through LDS, one column per lane (lanes 0..18)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = lq + 4 * i;
+        if (r < 6) {
+          if (lr < 6) sh[MO_H + 6 * r + lr] = Z11[i];
+          if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
+        }
+      }
+      __syncthreads();
       double E[6];
       const int cc = l < 19 ? l : 18;
 #pragma unroll
       for (int i = 0; i < 6; ++i) E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : sh[MO_G + 13 * i + (cc - 6)];
-      if (ABL & 2) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) E[i] *= 1e-3;
-      } else {
+      for (int p = 0; p < 6; ++p) {
+        double Pc[6];
 #pragma unroll
-        for (int p = 0; p < 6; ++p) {
-          double Pc[6];
+        for (int i = 0; i < 6; ++i) Pc[i] = readlane_f64(E[i], p);
+        const double inv = rcp_nr(Pc[p]);
+        const double ep = E[p] * inv;
 #pragma unroll
-          for (int i = 0; i < 6; ++i) Pc[i] = readlane_f64(E[i], p);
-          const double inv = rcp_nr(Pc[p]);
-          const double ep = E[p] * inv;
-#pragma unroll
-          for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
-        }
+        for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
       }
       if (l >= 6 && l < 19) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (l - 6)] = -E[i];
       }
+      __syncthreads();
+      V = mfma(sh[oK[0]], Z10[0], Z00);
+      V = mfma(sh[oK[1]], Z10[1], V);
+      kk[l] = sh[MO_KT + l];
+      if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
     }
-    __syncthreads();
-    // V~ <- Qxx + K~' G~
-    V = mfma(sh[oK[0]], Z10[0], Z00);
-    V = mfma(sh[oK[1]], Z10[1], V);
-    // K~ (78) and c_v (6) -> global for the forward rollout (each element loaded back by the
-    // same lane that stores it)
-    double* kk = KB + (long)k * KBUF_STRIDE;
-    kk[l] = sh[MO_KT + l];
-    if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
   }
 
   // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.

@@ -1,0 +1,93 @@
+"""GPU edge cases beyond the bench shapes: ragged horizons (N not a power of two, which takes
+k_linesearch's LDS-reduction path and short Riccati sweeps; N = 2 is the minimum), the other
+cost options of OSQPSolver (regularize=False, another dt / costs), batch sizes 0 and 1, and
+problems that differ wildly within one batch.  Each against the CPU oracle through the C-ABI.
+
+Tolerances as in test_gpu_parity.py: QP 1e-8 relative vs the exact KKT solve; full SQP 1e-6
+relative per problem with the alpha sequence and qp_iters identical.
+"""
+import numpy as np
+import pytest
+
+from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def _check_sqp(out, st, xcur, goals, XU, **kw):
+    for b in range(out.shape[0]):
+        sq = SQPRef(OSQPSolverRef(**kw))
+        ref = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        s = sq.get_stats()
+        assert st["qp_iters"][b] == s["qp_iters"]["values"][0], b
+        na = st["n_alphas"][b]
+        np.testing.assert_array_equal(st["alphas"][b][:na], s["linesearch_alphas"]["values"])
+        rel = np.linalg.norm(out[b] - ref) / np.linalg.norm(ref)
+        assert rel < 1e-6, (b, rel)
+
+
+@pytest.mark.parametrize("N", [2, 5, 20, 48])
+def test_ragged_horizon_qp_and_sqp(lib, model, N):
+    B = 3
+    xcur, goals, XU = synthetic_batch(B, N, seed=100 + N)
+    h = lib.Handle(model, N=N, max_batch=B)
+    XUp = XU + np.random.default_rng(N).normal(0, 0.2, XU.shape)
+    sol = h.qp(XUp, xcur, goals)
+    for b in range(B):
+        ref = OSQPSolverRef(N=N).setup_and_solve_qp(XUp[b], xcur[b], goals[b]).x
+        assert np.linalg.norm(sol[b] - ref) / np.linalg.norm(ref) < 1e-8
+        np.testing.assert_array_equal(sol[b][:12], xcur[b])
+    out, st = h.solve(xcur, goals, XU)
+    _check_sqp(out, st, xcur, goals, XU, N=N)
+
+
+def test_cost_options(lib, model):
+    N, B = 16, 3
+    kw = dict(N=N, dt=0.02, dQ_cost=0.05, R_cost=1e-4, QN_cost=50.0, regularize=False)
+    xcur, goals, XU = synthetic_batch(B, N, seed=5)
+    h = lib.Handle(model, max_batch=B, **kw)
+    out, st = h.solve(xcur, goals, XU)
+    _check_sqp(out, st, xcur, goals, XU, **kw)
+
+
+def test_batch_of_one_and_empty(lib, model):
+    N = 32
+    xcur, goals, XU = synthetic_batch(2, N, seed=9)
+    h = lib.Handle(model, N=N, max_batch=2)
+    out, st = h.solve(xcur[:1], goals[:1], XU[:1])
+    _check_sqp(out, st, xcur[:1], goals[:1], XU[:1], N=N)
+    e_out, e_st = h.solve(xcur[:0], goals[:0], XU[:0])
+    assert e_out.shape == (0, XU.shape[1]) and e_st.shape == (0,)
+
+
+def test_mixed_batch_extremes(lib, model):
+    """A batch mixing a start at rest on its goal, a start at the joint limits with large
+    velocities, and ordinary draws: each problem still equals its own oracle solve."""
+    from oracle import rbd
+
+    N, B = 32, 5
+    xcur, goals, XU = synthetic_batch(B, N, seed=21)
+    lim = rbd.params().q_upper
+    # problem 0: at rest exactly on its goal
+    g0 = rbd.eepos(xcur[0][:6])
+    goals[0] = np.tile(g0, N)
+    xcur[0][6:] = 0.0
+    # problem 1: near the position limits, fast
+    xcur[1][:6] = 0.95 * lim
+    xcur[1][6:] = np.array([2.0, -2.0, 1.5, -1.5, 3.0, -3.0])
+    for b in range(2):
+        XU[b] = 0.0
+        XU[b][:12] = xcur[b]
+    h = lib.Handle(model, N=N, max_batch=B)
+    out, st = h.solve(xcur, goals, XU)
+    assert np.isfinite(out).all()
+    _check_sqp(out, st, xcur, goals, XU, N=N)
