@@ -14,6 +14,7 @@
 
 #include "i7m_dynamics.h"
 #include "i7m_indy7_model.h"
+#include "i7m_sincos.h"
 
 namespace i7m {
 
@@ -44,7 +45,7 @@ struct ProblemStats {
 
 __device__ __forceinline__ void sincos6(const double* q, double c[6], double s[6]) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i) sincos(q[i], &s[i], &c[i]);
+  for (int i = 0; i < 6; ++i) sincos_q(q[i], &s[i], &c[i]);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
   double c[6], s[6];
   {
     double sj, cj;
-    sincos(X[j], &sj, &cj);
+    sincos_q(X[j], &sj, &cj);
     const int base = 6 * gg;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
