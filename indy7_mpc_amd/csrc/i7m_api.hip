@@ -65,11 +65,14 @@ struct i7m_handle {
   double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
   // I7M_QP_BOX (i7m_box.h): iterate, bound duals, Riccati inputs, predictor step; (max_batch, T)
   double *d_bx = nullptr, *d_bzl = nullptr, *d_bzu = nullptr, *d_bsig = nullptr, *d_bh = nullptr, *d_bdxa = nullptr;
+  double *d_bhinv = nullptr, *d_bdh = nullptr;  // per-stage H^-1 (max_batch, N-1, 36); corrector dh (max_batch, T)
   IpmState* d_bst = nullptr;
   int* d_bact = nullptr;
   uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
   int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
-  bool ipm_split = false;          // I7M_IPM=split: one launch per IPM phase instead of k_ipm_fused
+  // box QP: 1 k_ipm_fused<false> (default), 0 I7M_IPM=delta (k_ipm_fused<true>: the corrector
+  // reuses the predictor's factorisation; measured slower), 2 I7M_IPM=split
+  int ipm_mode = 1;
   int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
   bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
@@ -190,7 +193,7 @@ struct Bufs {
   double* kbuf;
   const double* fext;  // nullptr: no external wrench
   // box mode only (nullptr otherwise)
-  double *bx, *bzl, *bzu, *bsig, *bh, *bdxa;
+  double *bx, *bzl, *bzu, *bsig, *bh, *bdxa, *bhinv, *bdh;
   IpmState* bst;
   int* bact;
 };
@@ -199,7 +202,7 @@ Bufs bufs_at(const i7m_handle* h, long b0) {
   const long N = h->cfg.N, T = 18 * N - 6;
   Bufs W{h->d_lin + b0 * (N - 1) * LIN_STRIDE, h->d_cost + b0 * N * COST_STRIDE,
          h->d_qpd + b0 * (N - 1) * QPD_STRIDE, h->d_kbuf + b0 * (N - 1) * KBUF_STRIDE, h->has_fext ? h->d_fext + 6 * b0 : nullptr,
-         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (h->cfg.qp_mode == I7M_QP_BOX) {
     W.bx = h->d_bx + b0 * T;
     W.bzl = h->d_bzl + b0 * T;
@@ -207,6 +210,8 @@ Bufs bufs_at(const i7m_handle* h, long b0) {
     W.bsig = h->d_bsig + b0 * T;
     W.bh = h->d_bh + b0 * T;
     W.bdxa = h->d_bdxa + b0 * T;
+    W.bhinv = h->d_bhinv + b0 * (N - 1) * 36;
+    W.bdh = h->d_bdh + b0 * T;
     W.bst = h->d_bst + b0;
     W.bact = h->d_bact + b0;
   }
@@ -237,6 +242,12 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
                          W.kbuf, sol);
     else if (h->ablate == 1)
       hipExtLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
+    else if (h->ablate == 10)
+      hipExtLaunchKernelGGL(k_riccati_mfma<8>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                         sol, (const double*)nullptr, (const double*)nullptr);
+    else if (h->ablate == 11)
+      hipExtLaunchKernelGGL(k_riccati_mfma<24>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
                          sol, (const double*)nullptr, (const double*)nullptr);
     else if (h->ablate == 8)
       hipExtLaunchKernelGGL(k_riccati_mfma<4>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
@@ -293,10 +304,16 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   if (h->cfg.qp_mode != I7M_QP_BOX || P.B == 0) return I7M_OK;
   const BoxParams BP = box_params(h);
   const dim3 g(P.B), blk(64);
-  if (!h->ipm_split) {
+  if (h->ipm_mode != 2) {
     rc = timed(h, s, I7M_K_IPM_FUSED, [&](hipEvent_t ea, hipEvent_t eb) {
-      hipExtLaunchKernelGGL(k_ipm_fused, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd, active,
-                            W.kbuf, (const double*)sol, sol, W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst, W.bact);
+      if (h->ipm_mode == 0)
+        hipExtLaunchKernelGGL(k_ipm_fused<true>, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd,
+                              active, W.kbuf, (const double*)sol, sol, W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst,
+                              W.bact, W.bhinv, W.bdh);
+      else
+        hipExtLaunchKernelGGL(k_ipm_fused<false>, g, blk, 0, s, ea, eb, 0, h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd,
+                              active, W.kbuf, (const double*)sol, sol, W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst,
+                              W.bact, W.bhinv, W.bdh);
     });
     if (rc) return rc;
     *out = W.bx;
@@ -522,7 +539,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   // developer knob for A/B profiling of the two QP kernels (default: MFMA)
   if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
   if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
-  if (const char* e = std::getenv("I7M_IPM")) h->ipm_split = std::strcmp(e, "split") == 0;
+  if (const char* e = std::getenv("I7M_IPM"))
+    h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c)
@@ -548,6 +566,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     ok = alloc((void**)&h->d_bx, Bm * T * 8) && alloc((void**)&h->d_bzl, Bm * T * 8) &&
          alloc((void**)&h->d_bzu, Bm * T * 8) && alloc((void**)&h->d_bsig, Bm * T * 8) &&
          alloc((void**)&h->d_bh, Bm * T * 8) && alloc((void**)&h->d_bdxa, Bm * T * 8) &&
+         alloc((void**)&h->d_bhinv, Bm * (N - 1) * 36 * 8) && alloc((void**)&h->d_bdh, Bm * T * 8) &&
          alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
   std::vector<uint32_t> desc(RIC_DESC_WORDS);
@@ -570,7 +589,8 @@ void i7m_destroy(i7m_handle* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
                   h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc, h->d_qpd,
-                  h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact};
+                  h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact,
+                  h->d_bhinv, h->d_bdh};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& t : h->ev) {

@@ -11,6 +11,10 @@
 #include "i7m_kernels.h"
 #include "i7m_riccati_mfma.h"
 
+#ifndef I7M_IPM_WPE
+#define I7M_IPM_WPE 4
+#endif
+
 namespace i7m {
 
 struct BoxParams {
@@ -117,7 +121,8 @@ __device__ __forceinline__ IpmState ipm_init_body(const DevModel& M, const Solve
 __device__ __forceinline__ void ipm_pred_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
                                               const double* __restrict__ y, const double* __restrict__ x,
                                               const double* __restrict__ zl, const double* __restrict__ zu,
-                                              double* __restrict__ dxa, double* __restrict__ h, IpmState& S) {
+                                              double* __restrict__ dxa, double* __restrict__ h, IpmState& S,
+                                              double* __restrict__ dh = nullptr) {
   const int l = threadIdx.x;
   const long o = (long)b * P.T;
   double ap = 1.0, ad = 1.0;
@@ -156,6 +161,7 @@ __device__ __forceinline__ void ipm_pred_body(const DevModel& M, const SolvePara
       const double s = a / sl + c / su;
       hv = -a + c + (rl / sl - ru / su) - s * xv;
     }
+    if (dh) dh[o + e] = hv - h[o + e];  // the corrector's change of the linear terms
     h[o + e] = hv;
   }
   S.smu = smu;
@@ -276,17 +282,23 @@ __global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg
 }
 
 // The whole interior-point solve of one problem in one wavefront: init from the equality-QP
-// minimiser xeq, then predictor / corrector Newton steps (each a riccati_mfma_body<0, true> on
-// the problem's linearisation) until the problem converges or reaches max_iters.  One launch
-// per QP instead of 2 + 4 max_iters; each wave runs exactly its own iteration count and the
-// iteration state stays in registers.  Same arithmetic as the split kernels, phase for phase.
+// minimiser xeq, then predictor / corrector Newton steps until the problem converges or reaches
+// max_iters.  One launch per QP instead of 2 + 4 max_iters; each wave runs exactly its own
+// iteration count and the iteration state stays in registers.
+// !DELTA (default): both Newton steps are full Riccati solves, the same arithmetic as the split
+// kernels phase for phase.  DELTA (I7M_IPM=delta): the predictor step is a full
+// riccati_mfma_body<0, true, true> (which also stores every stage's H^-1) and the corrector
+// reuses that factorisation (riccati_delta_body: same Hessian, only the linear terms change by
+// dh).  Measured slower (14.7 vs 13.7 ms per QP at B = 4096, N = 64): the vector pass streams
+// as many bytes per stage as the full step and is as latency-bound.
 // Newton iterates go to y (B, T), the iterate to x.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
+template <bool DELTA>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_IPM_WPE, I7M_IPM_WPE)))
 k_ipm_fused(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP, const double* __restrict__ xu,
             const double* __restrict__ xs, const double* __restrict__ lin, const double* __restrict__ cost,
             const double* __restrict__ qpd, const int* __restrict__ active, double* __restrict__ kbuf,
             const double* __restrict__ xeq, double* y, double* x, double* zl, double* zu, double* sig, double* h,
-            double* dxa, IpmState* __restrict__ st, int* __restrict__ ipm_active) {
+            double* dxa, IpmState* __restrict__ st, int* __restrict__ ipm_active, double* hinv, double* dh) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
   __shared__ double sh[MO_TOTAL];
@@ -294,20 +306,26 @@ k_ipm_fused(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP, const 
   IpmState S = ipm_init_body(M, P, BP, b, xeq, x, zl, zu, sig, h);
   ipm_uniform(S);
   bool run = (active ? active[b] != 0 : true) && S.nb > 0;
-  // one Riccati call site (half 0: predictor, half 1: corrector) keeps one inlined copy
   // The lane id and the model pointer are laundered per step (an empty asm the compiler must
   // treat as redefining them), so the Riccati operand maps and the box bounds are rebuilt per
   // step instead of hoisted out of the loop and held live across it (which spills).
+  // !DELTA: one Riccati call site (half 0: predictor, half 1: corrector) keeps one inlined copy.
   for (int half = 0; run; half ^= 1) {
     int l = threadIdx.x;
     const DevModel* Mp = Mg;
     asm volatile("" : "+v"(l));
     asm volatile("" : "+s"(Mp));
     __syncthreads();
-    riccati_mfma_body<0, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l);
+    if (!DELTA) {
+      riccati_mfma_body<0, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l);
+    } else if (half == 0) {
+      riccati_mfma_body<0, true, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l, hinv);
+    } else {
+      riccati_delta_body(b, P, lin, kbuf, hinv, dh, y, sh, l);
+    }
     __syncthreads();
     if (half == 0) {
-      ipm_pred_body(*Mp, P, BP, b, y, x, zl, zu, dxa, h, S);
+      ipm_pred_body(*Mp, P, BP, b, y, x, zl, zu, dxa, h, S, DELTA ? dh : nullptr);
       ipm_uniform(S);
     } else {
       ipm_corr_body(*Mp, P, BP, b, y, x, zl, zu, dxa, sig, h, S);

@@ -66,7 +66,9 @@ __device__ __forceinline__ double rcp_nr(double d) {
 }
 
 // ABL (diagnostic builds only, results invalid): bit 0 skips the forward rollout, bit 1
-// replaces the Gauss-Jordan solve by a scaling; used to split the kernel's time.
+// replaces the Gauss-Jordan solve by a scaling, bit 3 sends every stage's kbuf traffic to stage
+// 0's slot (cache-resident), bit 4 the rollout's lin re-reads likewise; used to split the
+// kernel's time.
 // BOX: the interior-point Newton step of the box-constrained QP (oracle/box_ipm.py): the same
 // QP with Hessian P + diag(Sigma) and linear term g + h, Sigma and h given per variable in
 // bsig / bh (B, T).  The equality rows are unchanged, so the result is the Newton iterate
@@ -75,13 +77,16 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // 1024 SIMDs in one round.
 // The body of one problem's solve (problem b, one wavefront, lane l, `sh` = MO_TOTAL doubles of
 // LDS); k_riccati_mfma runs it once, k_ipm_fused (i7m_box.h) once per Newton step.
-template <int ABL, bool BOX>
+// HINV (box predictor steps): also carry the identity through the elimination and store H^-1
+// of every stage in hinv (B, N-1, 36) for riccati_delta_body (column-per-lane elimination).
+template <int ABL, bool BOX, bool HINV = false>
 __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
                                                   const double* __restrict__ xs, const double* __restrict__ lin,
                                                   const double* __restrict__ cost, const double* __restrict__ qpd,
                                                   double* __restrict__ kbuf, double* __restrict__ sol,
                                                   const double* __restrict__ bsig, const double* __restrict__ bh,
-                                                  double* __restrict__ sh, const int l) {
+                                                  double* __restrict__ sh, const int l,
+                                                  double* __restrict__ hinv = nullptr) {
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
   const double dt = P.dt;
@@ -220,8 +225,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     Z11 = mfma(bB[1], W1[2], Z11);
     d4 Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
-    double* kk = KB + (long)k * KBUF_STRIDE;
-    if (!(ABL & 4)) {
+    double* kk = KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE;
+    if (!(ABL & 4) && !BOX) {
       // K~ = -H^-1 G~ by Gauss-Jordan on [H | G~] (6 x 19) in place in the MFMA accumulator
       // layout: lane l holds column lr of rows lq and lq + 4 (lq < 2) of H (lr < 6) and of G~
       // (lr < 13).  Pivot p needs, per lane, M[r][p] of its two rows (published by the lanes
@@ -229,7 +234,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       // LDS slot, two writes and three broadcast-friendly reads, instead of 12 v_readlane per
       // pivot.  The arithmetic is the column-per-lane elimination's, operation for operation.
       // SPD H: no pivoting.  K~ ends where the V~ update wants it: the A operand of k-step s is
-      // K~[4s + lq][lr], i.e. this lane's G~ entry of row lq + 4s.
+      // K~[4s + lq][lr], i.e. this lane's G~ entry of row lq + 4s.  (The box variants keep the
+      // column-per-lane form below: fewer live registers next to their Sigma / h operand maps.)
       double eh0 = Z11[0], eh1 = Z11[1], eg0 = Z10[0], eg1 = Z10[1];
       if (ABL & 2) {
         eh0 *= 1e-3; eh1 *= 1e-3; eg0 *= 1e-3; eg1 *= 1e-3;
@@ -274,8 +280,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       if (l < 6) kk[78 + l] = sh[MO_CV + l];
     } else {
-      // (diagnostic A/B, I7M_ABLATE=8) column-per-lane Gauss-Jordan with v_readlane pivot
-      // broadcast: H, G~ through LDS, one column per lane (lanes 0..18)
+      // Column-per-lane Gauss-Jordan with v_readlane pivot broadcast (the box variants; for the
+      // plain QP a diagnostic A/B, I7M_ABLATE=8): H, G~ through LDS, one column of [H | G~] per
+      // lane (lanes 0..18); HINV adds the identity columns in lanes 19..24, which end as H^-1.
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = lq + 4 * i;
@@ -286,9 +293,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       __syncthreads();
       double E[6];
-      const int cc = l < 19 ? l : 18;
+      const int ncol = HINV ? 25 : 19;
+      const int cc = l < ncol ? l : ncol - 1;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : sh[MO_G + 13 * i + (cc - 6)];
+      for (int i = 0; i < 6; ++i)
+        E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : (cc < 19 ? sh[MO_G + 13 * i + (cc - 6)] : (i == cc - 19 ? 1.0 : 0.0));
 #pragma unroll
       for (int p = 0; p < 6; ++p) {
         double Pc[6];
@@ -302,6 +311,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       if (l >= 6 && l < 19) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (l - 6)] = -E[i];
+      }
+      if (HINV && l >= 19 && l < 25) {
+        double* hk = hinv + ((long)b * (N - 1) + k) * 36;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) hk[6 * i + (l - 19)] = E[i];
       }
       __syncthreads();
       V = mfma(sh[oK[0]], Z10[0], Z00);
@@ -324,7 +338,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
   const int ik = l < 6 ? l : 0;
   auto fsrc = [&](int k, int e) -> const double* {
-    return (e < KBUF_STRIDE) ? KB + (long)k * KBUF_STRIDE + e : LINb + (long)k * LIN_STRIDE + (e - KBUF_STRIDE);
+    return (e < KBUF_STRIDE) ? KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE + e : LINb + (long)((ABL & 16) ? 0 : k) * LIN_STRIDE + (e - KBUF_STRIDE);
   };
   double f[FD][3];
 #pragma unroll
@@ -396,6 +410,144 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
     xreg = nx;
     if (l < 12) S[18 * (k + 1) + l] = nx;
+  }
+}
+
+// The corrector Newton step of I7M_QP_BOX (k_ipm_fused): the QP of the last
+// riccati_mfma_body<0, true, true> run (same Hessian, dynamics and x_0) with its linear terms
+// changed by dh (B, T).  The KKT system is linear, so the new minimiser is the old one, y, plus
+// the minimiser of the change: a vector-only Riccati pass with that run's gains K (kbuf) and
+// H^-1 (hinv), zero dynamics offsets and zero initial state:
+//   p_{N-1} = dq_{N-1};  g_u = dr_k + B' p,  g_x = dq_k + A' p,  kff_k = -H^-1 g_u,  p <- g_x + K' g_u;
+//   du_k = K dx_k + kff_k,  dx_{k+1} = A dx_k + B du_k,  dx_0 = 0;   y += (dx, du).
+// No factorisation and no MFMA: ~1/4 of a full step.  kff overwrites kbuf's feedforward column.
+__device__ __forceinline__ void riccati_delta_body(const int b, const SolveParams& P, const double* __restrict__ lin,
+                                                   double* __restrict__ kbuf, const double* __restrict__ hinv,
+                                                   const double* __restrict__ dh, double* __restrict__ y,
+                                                   double* __restrict__ sh, const int l) {
+  const int N = P.N;
+  const double dt = P.dt;
+  const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
+  double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
+  const double* HB = hinv + (long)b * (N - 1) * 36;
+  const double* DH = dh + (long)b * P.T;
+  // backward stage slot: Aq | Av | Bu | K~ (78) | H^-1 (36) | dh_k (18);  then p (12), g_u (6)
+  enum { DA = 0, DV = 36, DB = 72, DK = 108, DI = 186, DD = 222, DP = 240, DG = 252 };
+  auto src = [&](int k, int e) -> const double* {
+    if (e < DK) return LINb + (long)k * LIN_STRIDE + e;
+    if (e < DI) return KB + (long)k * KBUF_STRIDE + (e - DK);
+    if (e < DD) return HB + (long)k * 36 + (e - DI);
+    return DH + 18 * k + (e - DD);
+  };
+  const int e3 = (l + 192 < DP) ? l + 192 : DP - 1;
+  double q0 = *src(N - 2, l), q1 = *src(N - 2, l + 64), q2 = *src(N - 2, l + 128), q3 = *src(N - 2, e3);
+  double preg = (l < 12) ? DH[18 * (N - 1) + l] : 0.0;  // p_{N-1} = dq of the terminal knot
+  const int c6 = (l < 6) ? l : (l < 12 ? l - 6 : 0);
+  const int cc = (l < 12) ? l : 0;
+  const int oa = (l < 6) ? DA : DV;  // g_x of lane c < 6 uses Aq' , of lane 6 + j Av'
+  for (int k = N - 2; k >= 0; --k) {
+    __syncthreads();
+    sh[l] = q0;
+    sh[l + 64] = q1;
+    sh[l + 128] = q2;
+    if (l + 192 < DP) sh[l + 192] = q3;
+    if (l < 12) sh[DP + l] = preg;
+    __syncthreads();
+    if (k > 0) { q0 = *src(k - 1, l); q1 = *src(k - 1, l + 64); q2 = *src(k - 1, l + 128); q3 = *src(k - 1, e3); }
+    // g_x (lanes 0..11): dq + [p_q + Aq' p_v ; dt p_q + Av' p_v];  g_u (lanes 0..5): dr + Bu' p_v
+    double gx = sh[DD + cc] + ((l < 6) ? preg : dt * sh[DP + c6]);
+    double gu = sh[DD + 12 + c6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double pv = sh[DP + 6 + i];
+      gx += sh[oa + 6 * i + c6] * pv;
+      gu += sh[DB + 6 * i + c6] * pv;
+    }
+    if (l < 6) sh[DG + l] = gu;
+    __syncthreads();
+    double g[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) g[m] = sh[DG + m];
+    double kf = 0.0;
+#pragma unroll
+    for (int n = 0; n < 6; ++n) kf -= sh[DI + 6 * c6 + n] * g[n];
+    if (l < 6) KB[(long)k * KBUF_STRIDE + 13 * l + 12] = kf;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) gx += sh[DK + 13 * m + cc] * g[m];
+    preg = gx;
+  }
+  // forward: as the main rollout (stage slot K~ 78 | c_v 6 | Aq Av Bu 108), c = 0, x_0 = 0, and
+  // the result added to y by the lanes that wrote y's entries
+  constexpr int FD = 2;
+  __syncthreads();  // kff stores -> loads below
+  double* Y = y + (long)b * P.T;
+  const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
+  const int ik = l < 6 ? l : 0;
+  auto fsrc = [&](int k, int e) -> const double* {
+    return (e < KBUF_STRIDE) ? KB + (long)k * KBUF_STRIDE + e : LINb + (long)k * LIN_STRIDE + (e - KBUF_STRIDE);
+  };
+  double f[FD][3];
+#pragma unroll
+  for (int d = 0; d < FD; ++d) {
+    const int kk = (d < N - 1) ? d : 0;
+    f[d][0] = *fsrc(kk, l);
+    f[d][1] = *fsrc(kk, l + 64);
+    f[d][2] = *fsrc(kk, l + 128);
+  }
+  double xreg = 0.0;
+  for (int k = 0; k < N - 1; ++k) {
+    __syncthreads();
+    sh[l] = f[0][0];
+    sh[l + 64] = f[0][1];
+    sh[l + 128] = f[0][2];
+#pragma unroll
+    for (int d = 0; d + 1 < FD; ++d) {
+      f[d][0] = f[d + 1][0];
+      f[d][1] = f[d + 1][1];
+      f[d][2] = f[d + 1][2];
+    }
+    const int kn = (k + FD < N - 1) ? k + FD : k;
+    f[FD - 1][0] = *fsrc(kn, l);
+    f[FD - 1][1] = *fsrc(kn, l + 64);
+    f[FD - 1][2] = *fsrc(kn, l + 128);
+    __syncthreads();
+    double r[19];
+    if (l < 6) {
+#pragma unroll
+      for (int j = 0; j < 13; ++j) r[j] = sh[13 * ik + j];
+#pragma unroll
+      for (int j = 13; j < 19; ++j) r[j] = 0.0;
+    } else {
+      r[0] = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        r[1 + j] = sh[84 + 6 * iv + j];
+        r[7 + j] = sh[84 + 36 + 6 * iv + j];
+        r[13 + j] = sh[84 + 72 + 6 * iv + j];
+      }
+    }
+    double X[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
+    double ua = r[12], ub = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
+    const double ureg = ua + ub;
+    if (l < 6) Y[18 * k + 12 + l] += ureg;
+    double U[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
+    double va = r[0], vb = 0.0, vc = 0.0, vq = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      va += r[1 + j] * X[j];
+      vb += r[7 + j] * X[6 + j];
+      vc += r[13 + j] * U[j];
+      vq = (l == j) ? X[6 + j] : vq;
+    }
+    const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
+    xreg = nx;
+    if (l < 12) Y[18 * (k + 1) + l] += nx;
   }
 }
 

@@ -46,8 +46,11 @@ def _qp_inputs(N, B, seed=46):
     return np.vstack([xcur, xcur]), np.vstack([goals, goals]), np.vstack([XU, XU2])
 
 
-@pytest.mark.parametrize("N", [16, 32])
-def test_box_qp_matches_oracle(lib, model, N):
+@pytest.mark.parametrize("N,ipm", [(16, None), (32, None), (32, "split"), (32, "delta")])
+def test_box_qp_matches_oracle(lib, model, N, ipm, monkeypatch):
+    """Default k_ipm_fused, and the split-launch and factorisation-reuse (delta) variants."""
+    if ipm:
+        monkeypatch.setenv("I7M_IPM", ipm)
     xcur, goals, XU = _qp_inputs(N, 3)
     B = XU.shape[0]
     h = _box_handle(lib, model, N, B)

@@ -1,6 +1,6 @@
-"""A/B of the config-4 interior-point paths on one GPU: k_ipm_fused (default) vs the split
-launches (I7M_IPM=split).  Same inputs; reports solves/s of each and whether the outputs are
-bit-identical.  python tools/config4_ab.py [--steps 3] [--B 4096] [--N 64]"""
+"""A/B of the config-4 interior-point paths on one GPU: k_ipm_fused<false> (default),
+k_ipm_fused<true> (I7M_IPM=delta: the corrector reuses the predictor's factorisation) and the
+split launches (I7M_IPM=split).  Same inputs; solves/s of each and the output difference vs split.  python tools/config4_ab.py [--steps 3] [--B 4096] [--N 64]"""
 import argparse
 import json
 import os
@@ -18,8 +18,8 @@ def run(mode, B, N, steps):
     from indy7_mpc_amd.model import default_model
     from indy7_mpc_amd.synthetic import make_batch
 
-    if mode == "split":
-        os.environ["I7M_IPM"] = "split"
+    if mode in ("split", "delta"):
+        os.environ["I7M_IPM"] = mode
     else:
         os.environ.pop("I7M_IPM", None)
     model = default_model()
@@ -60,10 +60,17 @@ def main():
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--N", type=int, default=64)
     a = ap.parse_args()
-    o1, r1 = run("fused", a.B, a.N, a.steps)
-    o2, r2 = run("split", a.B, a.N, a.steps)
-    print(json.dumps({"fused": r1, "split": r2, "bit_identical": bool(np.array_equal(o1, o2)),
-                      "max_abs_diff": float(np.abs(o1 - o2).max())}, indent=1), flush=True)
+    res, outs = {}, {}
+    for mode in ("fused", "delta", "split"):
+        outs[mode], res[mode] = run(mode, a.B, a.N, a.steps)
+        res[mode].pop("ipm_iters_hist")
+    ref = outs["split"]
+    for mode in ("fused", "delta"):
+        d = outs[mode] - ref
+        res[mode]["vs_split"] = {"bit_identical": bool(np.array_equal(outs[mode], ref)),
+                                 "max_abs_diff": float(np.abs(d).max()),
+                                 "max_rel_per_problem": float((np.linalg.norm(d, axis=1) / np.linalg.norm(ref, axis=1)).max())}
+    print(json.dumps(res, indent=1), flush=True)
 
 
 if __name__ == "__main__":
