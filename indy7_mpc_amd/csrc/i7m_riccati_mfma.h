@@ -58,6 +58,14 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// lane l <- lane l + 6 within each 16-lane row (DPP row_shl:6), fp64 as two 32-bit moves
+__device__ __forceinline__ double row_shl6_f64(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(bits & 0xffffffffLL), 0x106, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), 0x106, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // 1/d to full fp64 precision: v_rcp_f64 + two Newton steps.
 __device__ __forceinline__ double rcp_nr(double d) {
   double y = __builtin_amdgcn_rcp(d);
@@ -268,15 +276,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       // V~ <- Qxx + K~' G~
       V = mfma(ka0, Z10[0], Z00);
       V = mfma(ka1, Z10[1], V);
-      // K~ (78, row-major 6 x 13) and c_v (6) -> global for the forward rollout; stage 0 also
-      // stays in LDS (the rollout reads it from there)
+      // K~ (78, row-major 6 x 13) and c_v (6) -> global for the forward rollout
       if (lr < 13) {
         kk[13 * lq + lr] = ka0;
         if (lq < 2) kk[13 * (lq + 4) + lr] = ka1;
-        if (k == 0) {
-          sh[MO_KT + 13 * lq + lr] = ka0;
-          if (lq < 2) sh[MO_KT + 13 * (lq + 4) + lr] = ka1;
-        }
       }
       if (l < 6) kk[78 + l] = sh[MO_CV + l];
     } else {
@@ -328,65 +331,59 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
   // Lane l < 12 holds x_l and lane m < 6 holds u_m; every lane sees the full vectors through
   // v_readlane.  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
-  // (3 per lane) FD stages ahead into registers, dropped into one LDS slot, and each lane reads
-  // its own rows from there (lanes 0..5: a K~ row; lanes 6..11: c_v + Aq/Av/Bu rows).  Stage 0
-  // is still in LDS from the last backward step.
+  // (3 per lane) FD stages ahead into registers and dropped into one LDS slot permuted so that
+  // the 19 values each lane needs are contiguous: lane m < 6 the row m of K~ (13, then zeros),
+  // lane 6 + i c_v[i] and row i of Aq, Av, Bu; lanes >= 12 an all-zero block.  Every lane then
+  // reads its block with the same ds_read_b128 sequence (no divergent gathers).
   if (ABL & 1) return;
   constexpr int FD = 2;
+  constexpr int FB = 20;  // doubles per lane block
   __syncthreads();  // kbuf stores of the backward sweep -> loads below (same workgroup)
   double* S = sol + (long)b * P.T;
-  const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
-  const int ik = l < 6 ? l : 0;
   auto fsrc = [&](int k, int e) -> const double* {
-    return (e < KBUF_STRIDE) ? KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE + e : LINb + (long)((ABL & 16) ? 0 : k) * LIN_STRIDE + (e - KBUF_STRIDE);
+    return (e < KBUF_STRIDE) ? KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE + e
+                             : LINb + (long)((ABL & 16) ? 0 : k) * LIN_STRIDE + (e - KBUF_STRIDE);
   };
+  // slot position of stage element e
+  auto fpos = [](int e) -> int {
+    if (e < 78) return FB * (e / 13) + e % 13;
+    if (e < 84) return FB * (6 + e - 78);
+    const int t = e - 84, blk = t / 36, w = t % 36;
+    return FB * (6 + w / 6) + 1 + 6 * blk + w % 6;
+  };
+  const int w0 = fpos(l), w1 = fpos(l + 64), w2 = fpos(l + 128);
+  double* myb = sh + FB * (l < 12 ? l : 12);
+  // zero the slot once (K~ rows' tails and the spare block stay zero)
+  for (int e = l; e < FB * 13; e += 64) sh[e] = 0.0;
   double f[FD][3];
 #pragma unroll
   for (int d = 0; d < FD; ++d) {
-    const int kk = (1 + d < N - 1) ? 1 + d : 0;
+    const int kk = (d < N - 1) ? d : 0;
     f[d][0] = *fsrc(kk, l);
     f[d][1] = *fsrc(kk, l + 64);
     f[d][2] = *fsrc(kk, l + 128);
   }
   double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
   if (l < 12) S[l] = xreg;
-  int okt = MO_KT, ocv = MO_CV, oli = MO_AQ;  // stage-0 locations (backward stash)
   for (int k = 0; k < N - 1; ++k) {
-    if (k > 0) {
-      __syncthreads();
-      sh[l] = f[0][0];
-      sh[l + 64] = f[0][1];
-      sh[l + 128] = f[0][2];
+    __syncthreads();
+    sh[w0] = f[0][0];
+    sh[w1] = f[0][1];
+    sh[w2] = f[0][2];
 #pragma unroll
-      for (int d = 0; d + 1 < FD; ++d) {
-        f[d][0] = f[d + 1][0];
-        f[d][1] = f[d + 1][1];
-        f[d][2] = f[d + 1][2];
-      }
-      const int kn = (k + FD < N - 1) ? k + FD : k;
-      f[FD - 1][0] = *fsrc(kn, l);
-      f[FD - 1][1] = *fsrc(kn, l + 64);
-      f[FD - 1][2] = *fsrc(kn, l + 128);
-      okt = 0;
-      ocv = 78;
-      oli = 84;
-      __syncthreads();
+    for (int d = 0; d + 1 < FD; ++d) {
+      f[d][0] = f[d + 1][0];
+      f[d][1] = f[d + 1][1];
+      f[d][2] = f[d + 1][2];
     }
+    const int kn = (k + FD < N - 1) ? k + FD : k;
+    f[FD - 1][0] = *fsrc(kn, l);
+    f[FD - 1][1] = *fsrc(kn, l + 64);
+    f[FD - 1][2] = *fsrc(kn, l + 128);
+    __syncthreads();
     double r[19];
-    if (l < 6) {
 #pragma unroll
-      for (int j = 0; j < 13; ++j) r[j] = sh[okt + 13 * ik + j];
-#pragma unroll
-      for (int j = 13; j < 19; ++j) r[j] = 0.0;
-    } else {
-      r[0] = sh[ocv + iv];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        r[1 + j] = sh[oli + 6 * iv + j];
-        r[7 + j] = sh[oli + 36 + 6 * iv + j];
-        r[13 + j] = sh[oli + 72 + 6 * iv + j];
-      }
-    }
+    for (int j = 0; j < 19; ++j) r[j] = myb[j];
     double X[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
@@ -399,14 +396,15 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     double U[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
-    double va = r[0], vb = 0.0, vc = 0.0, vq = 0.0;
+    double va = r[0], vb = 0.0, vc = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       va += r[1 + j] * X[j];
       vb += r[7 + j] * X[6 + j];
       vc += r[13 + j] * U[j];
-      vq = (l == j) ? X[6 + j] : vq;
     }
+    // q lanes: q + dt v, v_l = x_{6+l} from lane l + 6 (DPP row shift, same 16-lane row)
+    const double vq = row_shl6_f64(xreg);
     const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
     xreg = nx;
     if (l < 12) S[18 * (k + 1) + l] = nx;
