@@ -17,6 +17,17 @@
 
 namespace i7m {
 
+// Workgroup barrier ordering LDS only (an LDS-scoped release / acquire around s_barrier, which
+// the compiler drops for the single-wave workgroups used here): unlike __syncthreads() it does
+// not wait for the wave's outstanding global stores (s_waitcnt vmcnt(0)), which no lane reads
+// back in the same phase.  Where another lane does read global data this wave wrote, the
+// kernels use __syncthreads().
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Device-side model: URDF numbers plus precomputed inertia about each joint origin.
 struct DevModel {
   double Rp[6][9];   // row-major

@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const bool pow2 = (N & (N - 1)) == 0;
   const double* goal = goals + (long)b * N * P.goal_stride + (long)(k < N ? k : 0) * P.goal_stride;
   const double* f6 = fext ? fext + 6L * b : nullptr;
-  __syncthreads();
+  lds_sync();
   // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
   auto reduce_store = [&](double o[4], int c0) {
     if (pow2) {
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       if (k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
     } else {
       part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
-      __syncthreads();
+      lds_sync();
       if (l < R && c0 + l < 1 + NALPHA) {
         double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
         for (int kk = 0; kk < N; ++kk) {
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         merit[c0 + l] = qc + vc + uc + P.mu * cv;
       }
     }
-    __syncthreads();
+    lds_sync();
   };
   int cstart = 0;
   if (lin) {
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R && cc < 1 + NALPHA; ++cc) {
       if (merit[cc] <= base) { found = cc; break; }
     }
-    __syncthreads();
+    lds_sync();
   }
   const double alpha = (found > 0) ? alphas[found - 1] : 0.0;
   if (mode == 1) {
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, S
                fext ? fext + 6L * b : nullptr, o);
     part[k][0] = o[0]; part[k][1] = o[1]; part[k][2] = o[2]; part[k][3] = o[3];
   }
-  __syncthreads();
+  lds_sync();
   if (l == 0) {
     double acc[4] = {0, 0, 0, 0};
     for (int k = 0; k < P.N; ++k)

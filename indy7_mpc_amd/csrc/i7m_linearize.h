@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) { my[4 + r] = Ib[r]; my[13 + r] = Ibd[r]; my[19 + r] = hV[r]; my[25 + r] = F0[r]; }
   }
-  __syncthreads();
+  lds_sync();
 
   // ---- 3. subtree sums for link j
   double cm = 0, ch[3] = {0, 0, 0}, cI[6] = {0, 0, 0, 0, 0, 0}, chd[3] = {0, 0, 0}, cId[6] = {0, 0, 0, 0, 0, 0};
@@ -283,14 +283,14 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) ej[r] = bj[r] - cj[r];
   }
-  __syncthreads();  // everyone has read the phase-1 slots
+  lds_sync();  // everyone has read the phase-1 slots
   // publish a_j, e_j, S_j for the M row and the derivative columns
   if (g < KPW) {
 #pragma unroll
     for (int r = 0; r < 6; ++r) { my[r] = aj[r]; my[6 + r] = ej[r]; my[12 + r] = Sj[r]; }
     st0[gg][j] = tau0;
   }
-  __syncthreads();
+  lds_sync();
   // M row j: M_jk = a_j . S_k (k <= j)
   if (g < KPW) {
 #pragma unroll
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
       }
     }
   }
-  __syncthreads();
+  lds_sync();
 
   // ---- 4. a = M^-1 (u - tau0) (every lane), dA_j = sum_{i<=j} S_i a_i, g_j = I_j dA_j
   double L[6][6], acc[6];
@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) my[18 + r] = gI[r];
   }
-  __syncthreads();
+  lds_sync();
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (i >= j) {
@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
         my[24 + r] = aq * qj + av * v[j] + bu * uj;
       }
     }
-    __syncthreads();
+    lds_sync();
     if (dyn) {
       double sacc = 0.0;
 #pragma unroll

@@ -180,28 +180,35 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
     }
   }
-  __syncthreads();
+  lds_sync();
   d4 V;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) V[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
+  for (int i = 0; i < 4; ++i) V[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
 
   constexpr int SE = BOX ? 176 : 140;  // stash length
-  auto src = [&](int k, int e) -> const double* {
-    if (e < MO_QP) return LINb + (long)k * LIN_STRIDE + e;
-    if (e < MO_SIG) return QB + (long)k * QPD_STRIDE + (e - MO_QP);
-    if (e < MO_HB) return bsig + (long)b * P.T + 18 * k + (e - MO_SIG);
-    return bh + (long)b * P.T + 18 * k + (e - MO_HB);
+  // stash element e of stage k lives at base(e) + k * stride(e): resolved once per lane for its
+  // three elements, so the per-stage loads are one multiply-add each (no divergent selects)
+  auto base_of = [&](int e, int& stride) -> const double* {
+    if (e < MO_QP) { stride = LIN_STRIDE; return LINb + e; }
+    if (e < MO_SIG) { stride = QPD_STRIDE; return QB + (e - MO_QP); }
+    stride = 18;
+    if (e < MO_HB) return bsig + (long)b * P.T + (e - MO_SIG);
+    return bh + (long)b * P.T + (e - MO_HB);
   };
   const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
-  double p0 = *src(N - 2, l), p1 = *src(N - 2, l + 64), p2 = *src(N - 2, e2);
+  int st0, st1, st2;
+  const double* sb0 = base_of(l, st0);
+  const double* sb1 = base_of(l + 64, st1);
+  const double* sb2 = base_of(e2, st2);
+  double p0 = sb0[(long)(N - 2) * st0], p1 = sb1[(long)(N - 2) * st1], p2 = sb2[(long)(N - 2) * st2];
 
   for (int k = N - 2; k >= 0; --k) {
-    __syncthreads();
+    lds_sync();
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
     if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
-    __syncthreads();
-    if (k > 0) { p0 = *src(k - 1, l); p1 = *src(k - 1, l + 64); p2 = *src(k - 1, e2); }
+    lds_sync();
+    if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
     double bA[4], bB[2];
 #pragma unroll
     for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
@@ -210,9 +217,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     d4 Qi, Ri, Ni;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      Qi[i] = sh[q1[i]] * sh[q2[i]] + (BOX ? sh[oS[i]] : 0.0);
-      Ri[i] = sh[oR[i]] + (BOX ? sh[oR2[i]] : 0.0);
-      Ni[i] = sh[oN[i]] + (BOX ? sh[oN2[i]] : 0.0);
+      // (x + 0.0 is not folded for doubles: the box shifts are added only in BOX builds)
+      Qi[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
+      Ri[i] = BOX ? sh[oR[i]] + sh[oR2[i]] : sh[oR[i]];
+      Ni[i] = BOX ? sh[oN[i]] + sh[oN2[i]] : sh[oN[i]];
     }
     // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
     // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
@@ -260,7 +268,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
             row[2 * lr] = (p >> 2) ? eh1 : eh0;
             row[2 * lr + 1] = (p >> 2) ? eg1 : eg0;
           }
-          __syncthreads();
+          lds_sync();
           const double mr0 = col[2 * lq], mr1 = col[2 * lq + 1];
           const double mph = row[2 * lr], mpg = row[2 * lr + 1];
           const double inv = rcp_nr(row[2 * p]);
@@ -294,7 +302,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
           if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
         }
       }
-      __syncthreads();
+      lds_sync();
       double E[6];
       const int ncol = HINV ? 25 : 19;
       const int cc = l < ncol ? l : ncol - 1;
@@ -320,7 +328,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
         for (int i = 0; i < 6; ++i) hk[6 * i + (l - 19)] = E[i];
       }
-      __syncthreads();
+      lds_sync();
       V = mfma(sh[oK[0]], Z10[0], Z00);
       V = mfma(sh[oK[1]], Z10[1], V);
       kk[l] = sh[MO_KT + l];
@@ -366,7 +374,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
   if (l < 12) S[l] = xreg;
   for (int k = 0; k < N - 1; ++k) {
-    __syncthreads();
+    lds_sync();
     sh[w0] = f[0][0];
     sh[w1] = f[0][1];
     sh[w2] = f[0][2];
@@ -380,7 +388,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     f[FD - 1][0] = *fsrc(kn, l);
     f[FD - 1][1] = *fsrc(kn, l + 64);
     f[FD - 1][2] = *fsrc(kn, l + 128);
-    __syncthreads();
+    lds_sync();
     double r[19];
 #pragma unroll
     for (int j = 0; j < 19; ++j) r[j] = myb[j];
@@ -444,13 +452,13 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   const int cc = (l < 12) ? l : 0;
   const int oa = (l < 6) ? DA : DV;  // g_x of lane c < 6 uses Aq' , of lane 6 + j Av'
   for (int k = N - 2; k >= 0; --k) {
-    __syncthreads();
+    lds_sync();
     sh[l] = q0;
     sh[l + 64] = q1;
     sh[l + 128] = q2;
     if (l + 192 < DP) sh[l + 192] = q3;
     if (l < 12) sh[DP + l] = preg;
-    __syncthreads();
+    lds_sync();
     if (k > 0) { q0 = *src(k - 1, l); q1 = *src(k - 1, l + 64); q2 = *src(k - 1, l + 128); q3 = *src(k - 1, e3); }
     // g_x (lanes 0..11): dq + [p_q + Aq' p_v ; dt p_q + Av' p_v];  g_u (lanes 0..5): dr + Bu' p_v
     double gx = sh[DD + cc] + ((l < 6) ? preg : dt * sh[DP + c6]);
@@ -462,7 +470,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
       gu += sh[DB + 6 * i + c6] * pv;
     }
     if (l < 6) sh[DG + l] = gu;
-    __syncthreads();
+    lds_sync();
     double g[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m) g[m] = sh[DG + m];
@@ -494,7 +502,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   }
   double xreg = 0.0;
   for (int k = 0; k < N - 1; ++k) {
-    __syncthreads();
+    lds_sync();
     sh[l] = f[0][0];
     sh[l + 64] = f[0][1];
     sh[l + 128] = f[0][2];
@@ -508,7 +516,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
     f[FD - 1][0] = *fsrc(kn, l);
     f[FD - 1][1] = *fsrc(kn, l + 64);
     f[FD - 1][2] = *fsrc(kn, l + 128);
-    __syncthreads();
+    lds_sync();
     double r[19];
     if (l < 6) {
 #pragma unroll
