@@ -292,50 +292,78 @@ __global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg
 // dh).  Measured slower (14.7 vs 13.7 ms per QP at B = 4096, N = 64): the vector pass streams
 // as many bytes per stage as the full step and is as latency-bound.
 // Newton iterates go to y (B, T), the iterate to x.
+// Everything k_ipm_fused reads, passed as one kernel argument.  The kernel re-reads it from the
+// kernarg segment through a laundered scalar pointer in every Newton step, so the ~20 buffer
+// pointers are reloaded (s_load, scalar cache) where used instead of pinned in SGPRs across the
+// whole loop (which spilled them into VGPR lanes, and VGPRs to scratch).
+struct IpmFusedArgs {
+  const DevModel* Mg;
+  SolveParams P;
+  BoxParams BP;
+  const double *xu, *xs, *lin, *cost, *qpd;
+  const int* active;
+  double* kbuf;
+  const double* xeq;
+  double *y, *x, *zl, *zu, *sig, *h, *dxa;
+  IpmState* st;
+  int* ipm_active;
+  double *hinv, *dh;
+};
+// the kernarg segment, laundered (the cast back to a generic pointer is inferred to the
+// constant address space again, so the fields are scalar loads)
+__device__ __forceinline__ const IpmFusedArgs* kernarg_ipm() {
+  auto p = __builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (const IpmFusedArgs*)p;
+}
+
 template <bool DELTA>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_IPM_WPE, I7M_IPM_WPE)))
-k_ipm_fused(const DevModel* __restrict__ Mg, SolveParams P, BoxParams BP, const double* __restrict__ xu,
-            const double* __restrict__ xs, const double* __restrict__ lin, const double* __restrict__ cost,
-            const double* __restrict__ qpd, const int* __restrict__ active, double* __restrict__ kbuf,
-            const double* __restrict__ xeq, double* y, double* x, double* zl, double* zu, double* sig, double* h,
-            double* dxa, IpmState* __restrict__ st, int* __restrict__ ipm_active, double* hinv, double* dh) {
+k_ipm_fused(IpmFusedArgs args) {
   const int b = blockIdx.x;
-  if (b >= P.B) return;
+  if (b >= args.P.B) return;
   __shared__ double sh[MO_TOTAL];
-  const DevModel& M = *Mg;
-  IpmState S = ipm_init_body(M, P, BP, b, xeq, x, zl, zu, sig, h);
-  ipm_uniform(S);
-  bool run = (active ? active[b] != 0 : true) && S.nb > 0;
-  // The lane id and the model pointer are laundered per step (an empty asm the compiler must
-  // treat as redefining them), so the Riccati operand maps and the box bounds are rebuilt per
-  // step instead of hoisted out of the loop and held live across it (which spills).
+  IpmState S;
+  bool run;
+  {
+    const IpmFusedArgs& a = args;
+    S = ipm_init_body(*a.Mg, a.P, a.BP, b, a.xeq, a.x, a.zl, a.zu, a.sig, a.h);
+    ipm_uniform(S);
+    run = (a.active ? a.active[b] != 0 : true) && S.nb > 0;
+  }
+  // The lane id and the argument pointer are laundered per step (an empty asm the compiler must
+  // treat as redefining them): the Riccati operand maps, the box bounds and the buffer pointers
+  // are rebuilt / reloaded per step instead of hoisted out of the loop and held live across it.
   // !DELTA: one Riccati call site (half 0: predictor, half 1: corrector) keeps one inlined copy.
   for (int half = 0; run; half ^= 1) {
     int l = threadIdx.x;
-    const DevModel* Mp = Mg;
+    const IpmFusedArgs* A = kernarg_ipm();
     asm volatile("" : "+v"(l));
-    asm volatile("" : "+s"(Mp));
+    const SolveParams P = A->P;
     __syncthreads();
     if (!DELTA) {
-      riccati_mfma_body<0, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l);
+      riccati_mfma_body<0, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l);
     } else if (half == 0) {
-      riccati_mfma_body<0, true, true>(b, P, xu, xs, lin, cost, qpd, kbuf, y, sig, h, sh, l, hinv);
+      riccati_mfma_body<0, true, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
+                                       A->hinv);
     } else {
-      riccati_delta_body(b, P, lin, kbuf, hinv, dh, y, sh, l);
+      riccati_delta_body(b, P, A->lin, A->kbuf, A->hinv, A->dh, A->y, sh, l);
     }
     __syncthreads();
+    const IpmFusedArgs* B = kernarg_ipm();
+    const BoxParams BP = B->BP;
     if (half == 0) {
-      ipm_pred_body(*Mp, P, BP, b, y, x, zl, zu, dxa, h, S, DELTA ? dh : nullptr);
+      ipm_pred_body(*B->Mg, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
       ipm_uniform(S);
     } else {
-      ipm_corr_body(*Mp, P, BP, b, y, x, zl, zu, dxa, sig, h, S);
+      ipm_corr_body(*B->Mg, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->sig, B->h, S);
       ipm_uniform(S);
       run = !ipm_done(S, BP);
     }
   }
   if (threadIdx.x == 0) {
-    st[b] = S;
-    ipm_active[b] = 0;
+    args.st[b] = S;
+    args.ipm_active[b] = 0;
   }
 }
 
