@@ -99,7 +99,10 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
     }
   }
 
-  // ---- 1. serial chain (every lane): world placement of each joint, S, V, A0 (qdd = 0)
+  // ---- 1. serial chain: world placement of each joint, S, V, A0 (qdd = 0).  Lane j runs the
+  // chain up to its own link (the updates of links i > j are masked off), so its registers end
+  // holding link j's values with no per-link copies; the end-effector position comes from the
+  // knot's link-5 lane.
   double Rj[9], pj[3], Sj[6], Vj[6], A0j[6], pE[3];
   {
     double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
@@ -108,45 +111,50 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
     double A[6] = {-Md.g[0], -Md.g[1], -Md.g[2], 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const double* Rp = Md.Rp[i];
-      const double* t = Md.tp[i];
-      double np_[3], RR[9];
+      if (i <= j) {
+        const double* Rp = Md.Rp[i];
+        const double* t = Md.tp[i];
+        double np_[3], RR[9];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[3 * r] * t[0] + R[3 * r + 1] * t[1] + R[3 * r + 2] * t[2];
+        for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[3 * r] * t[0] + R[3 * r + 1] * t[1] + R[3 * r + 2] * t[2];
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int qq = 0; qq < 3; ++qq) RR[3 * r + qq] = R[3 * r] * Rp[qq] + R[3 * r + 1] * Rp[3 + qq] + R[3 * r + 2] * Rp[6 + qq];
+          for (int qq = 0; qq < 3; ++qq) RR[3 * r + qq] = R[3 * r] * Rp[qq] + R[3 * r + 1] * Rp[3 + qq] + R[3 * r + 2] * Rp[6 + qq];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        R[3 * r] = RR[3 * r] * c[i] + RR[3 * r + 1] * s[i];
-        R[3 * r + 1] = RR[3 * r + 1] * c[i] - RR[3 * r] * s[i];
-        R[3 * r + 2] = RR[3 * r + 2];
-        p[r] = np_[r];
-      }
-      // S = (p x z; z), z = R[:,2]
-      double S[6];
-      S[3] = R[2]; S[4] = R[5]; S[5] = R[8];
-      S[0] = p[1] * S[5] - p[2] * S[4];
-      S[1] = p[2] * S[3] - p[0] * S[5];
-      S[2] = p[0] * S[4] - p[1] * S[3];
+        for (int r = 0; r < 3; ++r) {
+          R[3 * r] = RR[3 * r] * c[i] + RR[3 * r + 1] * s[i];
+          R[3 * r + 1] = RR[3 * r + 1] * c[i] - RR[3 * r] * s[i];
+          R[3 * r + 2] = RR[3 * r + 2];
+          p[r] = np_[r];
+        }
+        // S = (p x z; z), z = R[:,2]
+        double S[6];
+        S[3] = R[2]; S[4] = R[5]; S[5] = R[8];
+        S[0] = p[1] * S[5] - p[2] * S[4];
+        S[1] = p[2] * S[3] - p[0] * S[5];
+        S[2] = p[0] * S[4] - p[1] * S[3];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) V[r] += S[r] * v[i];
-      double VS[6];
-      mcross(V, S, VS);
+        for (int r = 0; r < 6; ++r) V[r] += S[r] * v[i];
+        double VS[6];
+        mcross(V, S, VS);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) A[r] += VS[r] * v[i];
-      if (i == j) {
-#pragma unroll
-        for (int r = 0; r < 9; ++r) Rj[r] = R[r];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) pj[r] = p[r];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) { Sj[r] = S[r]; Vj[r] = V[r]; A0j[r] = A[r]; }
+        for (int r = 0; r < 6; ++r) A[r] += VS[r] * v[i];
       }
     }
 #pragma unroll
-    for (int r = 0; r < 3; ++r) pE[r] = p[r];  // joint-6 origin = the end effector
+    for (int r = 0; r < 9; ++r) Rj[r] = R[r];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) pj[r] = p[r];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { Vj[r] = V[r]; A0j[r] = A[r]; }
+    Sj[3] = R[2]; Sj[4] = R[5]; Sj[5] = R[8];
+    Sj[0] = p[1] * Sj[5] - p[2] * Sj[4];
+    Sj[1] = p[2] * Sj[3] - p[0] * Sj[5];
+    Sj[2] = p[0] * Sj[4] - p[1] * Sj[3];
+    // joint-6 origin = the end effector: from the knot's link-5 lane
+#pragma unroll
+    for (int r = 0; r < 3; ++r) pE[r] = __shfl(p[r], 6 * gg + 5, 64);
   }
 
   double jte = 0.0, wreg = 1.0;  // (J^T e)_j and the cost regularisation weight of this knot
