@@ -120,6 +120,63 @@ inline size_t ls_lds_bytes(int T) {
   const int park = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
   return sizeof(double) * (size_t)((LS_STAGE ? 2 * T : 0) + park);
 }
+// Merit terms of one (candidate, knot) lane of k_linesearch: qcost, vcost, ucost and the
+// integrator error (src/osqp_sqp.py:13-47) at the line-search point XU + al (sol - XU)
+// (src/osqp_sqp.py:60), from the LDS copies of XU / sol; the knot values are re-read from LDS
+// where used instead of being held in registers across the dynamics.  (As a separate inlined
+// function the kernel allocates spill-free at 249 VGPRs; written in the round loop it spilled,
+// 115 -> 110 us.)
+template <bool SPEC>
+__device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, const SolveParams& P, const int k,
+                                                      const bool last, const bool base_pt, const double al,
+                                                      const double* sX, const double* sS, const double* goal,
+                                                      const double* f6, double* fpark, double* o) {
+  const DevModel& Md = SPEC ? kIndy7Model : *Mg;
+  const int ok = 18 * k, on = 18 * (last ? k : k + 1);
+  auto val = [&](int e) -> double {
+    const double xv = sX[e];
+    return base_pt ? xv : xv + al * (sS[e] - xv);
+  };
+  double c[6], sn[6], pe[3];
+  {
+    double q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = val(ok + i);
+    sincos6(q, c, sn);
+  }
+  fk_jac(Md, c, sn, pe, nullptr);
+  const double e0 = pe[0] - goal[0], e1 = pe[1] - goal[1], e2 = pe[2] - goal[2];
+  o[0] = (last ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
+  double vv = 0.0, uu = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double vi = val(ok + 6 + i);
+    vv += vi * vi;
+  }
+  o[1] = P.dQ * vv;
+  if (!last) {
+    double v[6], u[6], L[6][6], a[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      v[i] = val(ok + 6 + i);
+      u[i] = val(ok + 12 + i);
+      uu += u[i] * u[i];
+    }
+    o[2] = P.R * uu;
+    forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark);
+    asm volatile("" ::: "memory");  // re-read the knot values from LDS below
+    double eq = 0.0, ev = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double dq = (val(ok + i) + val(ok + 6 + i) * P.dt) - val(on + i);
+      const double dv = (val(ok + 6 + i) + a[i] * P.dt) - val(on + 6 + i);
+      eq += dq * dq;
+      ev += dv * dv;
+    }
+    o[3] = sqrt(eq) + sqrt(ev);
+  }
+}
+
 template <bool SPEC, int ABL = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    double* __restrict__ xu, const double* __restrict__ sol,
@@ -236,44 +293,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
         o[3] = val(on + 6) + val(ok + 11);
       } else {
-        double c[6], sn[6], pe[3];
-        {
-          double q[6];
-#pragma unroll
-          for (int i = 0; i < 6; ++i) q[i] = val(ok + i);
-          sincos6(q, c, sn);
-        }
-        fk_jac(Md, c, sn, pe, nullptr);
-        const double e0 = pe[0] - goal[0], e1 = pe[1] - goal[1], e2 = pe[2] - goal[2];
-        o[0] = (last ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
-        double vv = 0.0, uu = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const double vi = val(ok + 6 + i);
-          vv += vi * vi;
-        }
-        o[1] = P.dQ * vv;
-        if (!last) {
-          double v[6], u[6], L[6][6], a[6];
-#pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            v[i] = val(ok + 6 + i);
-            u[i] = val(ok + 12 + i);
-            uu += u[i] * u[i];
-          }
-          o[2] = P.R * uu;
-          forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark + l);
-          asm volatile("" ::: "memory");  // re-read the knot values from LDS below
-          double eq = 0.0, ev = 0.0;
-#pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            const double dq = (val(ok + i) + val(ok + 6 + i) * P.dt) - val(on + i);
-            const double dv = (val(ok + 6 + i) + a[i] * P.dt) - val(on + 6 + i);
-            eq += dq * dq;
-            ev += dv * dv;
-          }
-          o[3] = sqrt(eq) + sqrt(ev);
-        }
+        ls_merit_terms<SPEC>(Mg, P, k, last, base_pt, al, sX, sS, goal, f6, fpark + l, o);
       }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
