@@ -114,12 +114,17 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // waves per CU.  Measured 151 -> 132 us (1 wave/SIMD before); staging matters more than the
 // ~90 B/lane of spill the 2-wave target leaves.
 constexpr int LS_NLDS = 3;  // links whose RNEA forces k_linesearch parks in LDS
-constexpr bool LS_STAGE = true;  // stage XU / sol in LDS (else read them through the caches)
 // dynamic LDS of k_linesearch for trajectory length T
 inline size_t ls_lds_bytes(int T) {
   const int park = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
-  return sizeof(double) * (size_t)((LS_STAGE ? 2 * T : 0) + park);
+  return sizeof(double) * (size_t)(2 * T + park);
 }
+// A trajectory entry staged for the line search: XU and the QP step sol - XU side by side, so
+// a line-search point x + al d is one 16-byte LDS read.
+struct alignas(16) XD {
+  double x, d;
+};
+
 // Merit terms of one (candidate, knot) lane of k_linesearch: qcost, vcost, ucost and the
 // integrator error (src/osqp_sqp.py:13-47) at the line-search point XU + al (sol - XU)
 // (src/osqp_sqp.py:60), from the LDS copies of XU / sol; the knot values are re-read from LDS
@@ -129,13 +134,13 @@ inline size_t ls_lds_bytes(int T) {
 template <bool SPEC>
 __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, const SolveParams& P, const int k,
                                                       const bool last, const bool base_pt, const double al,
-                                                      const double* sX, const double* sS, const double* goal,
+                                                      const XD* sXD, const double* goal,
                                                       const double* f6, double* fpark, double* o) {
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   const int ok = 18 * k, on = 18 * (last ? k : k + 1);
   auto val = [&](int e) -> double {
-    const double xv = sX[e];
-    return base_pt ? xv : xv + al * (sS[e] - xv);
+    const XD p = sXD[e];
+    return base_pt ? p.x : p.x + al * p.d;
   };
   double c[6], sn[6], pe[3];
   {
@@ -197,18 +202,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   double* X = xu + (long)b * P.T;
   const double* S = sol + (long)b * P.T;
   // the problem's XU and QP minimiser, staged once in LDS for every round
-  // dynamic LDS (ls_lds_bytes): sX | sS (T each) | RNEA link-force parking (rnea NLDS), which
+  // dynamic LDS (ls_lds_bytes): (XU, sol - XU) pairs (T) | RNEA link-force parking (rnea NLDS), which
   // also holds the non-power-of-2 reduction (a different phase of each round)
-  extern __shared__ double ls_dyn[];
-  const double* sX = LS_STAGE ? ls_dyn : X;
-  const double* sS = LS_STAGE ? ls_dyn + P.T : S;
-  double* fpark = ls_dyn + (LS_STAGE ? 2 * P.T : 0);
+  extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
+  XD* sXD = reinterpret_cast<XD*>(ls_dyn);
+  double* fpark = ls_dyn + 2 * P.T;
   double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
   __shared__ double merit[9];
-  if (LS_STAGE) {
+  {
     for (int e = l; e < P.T; e += 64) {
-      ls_dyn[e] = X[e];
-      ls_dyn[P.T + e] = S[e];
+      const double xv = X[e];
+      sXD[e] = XD{xv, S[e] - xv};
     }
   }
   const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
@@ -254,14 +258,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       o[0] = CB[k * COST_STRIDE + 6] * (nrm * nrm);
       double vv = 0.0, uu = 0.0, eq = 0.0, ev = 0.0;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) vv += sX[ok + 6 + i] * sX[ok + 6 + i];
+      for (int i = 0; i < 6; ++i) vv += sXD[ok + 6 + i].x * sXD[ok + 6 + i].x;
       o[1] = P.dQ * vv;
       if (!last) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          uu += sX[ok + 12 + i] * sX[ok + 12 + i];
-          const double dq = (sX[ok + i] + sX[ok + 6 + i] * P.dt) - sX[on + i];
-          const double dv = (sX[ok + 6 + i] + LB[k * LIN_STRIDE + 108 + i] * P.dt) - sX[on + 6 + i];
+          uu += sXD[ok + 12 + i].x * sXD[ok + 12 + i].x;
+          const double dq = (sXD[ok + i].x + sXD[ok + 6 + i].x * P.dt) - sXD[on + i].x;
+          const double dv = (sXD[ok + 6 + i].x + LB[k * LIN_STRIDE + 108 + i] * P.dt) - sXD[on + 6 + i].x;
           eq += dq * dq;
           ev += dv * dv;
         }
@@ -286,21 +290,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const double al = base_pt ? 0.0 : alphas[cand - 1];
       const int ok = 18 * k, on = 18 * (last ? k : k + 1);
       auto val = [&](int e) -> double {
-        const double xv = sX[e];
-        return base_pt ? xv : xv + al * (sS[e] - xv);
+        const XD p = sXD[e];
+        return base_pt ? p.x : p.x + al * p.d;
       };
       if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
         o[3] = val(on + 6) + val(ok + 11);
       } else {
-        ls_merit_terms<SPEC>(Mg, P, k, last, base_pt, al, sX, sS, goal, f6, fpark + l, o);
+        ls_merit_terms<SPEC>(Mg, P, k, last, base_pt, al, sXD, goal, f6, fpark + l, o);
       }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
         double dd = 0.0;
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-          const double t = val(i) - sX[i];
+          const double t = val(i) - sXD[i].x;
           dd += t * t;
         }
         o[3] += sqrt(dd);
@@ -331,8 +335,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   double ss = 0.0;
   for (int e = l; e < P.T; e += 64) {
-    const double xv = sX[e];
-    const double stp = alpha * (sS[e] - xv);
+    const XD p = sXD[e];
+    const double xv = p.x;
+    const double stp = alpha * p.d;
     X[e] = xv + stp;
     ss += stp * stp;
   }
