@@ -131,7 +131,8 @@ int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur,
               int32_t goal_stride, double* xu_out, i7m_problem_stats* stats);
 
 /* Full SQP solve on device-resident buffers, asynchronous on the handle's stream.
- * d_stats may be NULL. xu_in may alias xu_out (in-place). */
+ * d_stats may be NULL. xu_in may alias xu_out (in-place); otherwise xu_in is only read and every
+ * row of xu_out is written (no staging copy). */
 int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const double* d_xcur,
                      const double* d_goals, int32_t goal_stride, double* d_xu_out,
                      i7m_problem_stats* d_stats);

@@ -80,7 +80,7 @@ struct i7m_handle {
   // hipGraph replay of run_sqp (run_sqp_graphed): a few instantiated graphs keyed by the call
   struct GraphEntry {
     int B, goal_stride, has_fext;
-    const void *xu, *xs, *goals, *st, *stream;
+    const void *xu_in, *xu, *xs, *goals, *st, *stream;
     hipGraphExec_t exec;
     unsigned long long last_use;
   };
@@ -218,18 +218,21 @@ Bufs bufs_at(const i7m_handle* h, long b0) {
   return W;
 }
 
+// init_active / init_stats (first SQP iteration only): the kernel marks every problem active
+// and zeroes its stats, so a solve needs no separate memset launches.
 int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
-                     const double* goals, const int* active) {
+                     const double* goals, const int* active, int* init_active = nullptr,
+                     ProblemStats* init_stats = nullptr) {
   const long knots = (long)P.B * P.N;
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
   return timed(h, s, I7M_K_LIN, [&](hipEvent_t ea, hipEvent_t eb) {
     if (h->spec)
       hipExtLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost, W.qpd);
+                         W.lin, W.cost, W.qpd, init_active, init_stats);
     else
       hipExtLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost, W.qpd);
+                         W.lin, W.cost, W.qpd, init_active, init_stats);
   });
 }
 
@@ -263,22 +266,23 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
 
 // base_from_lin: lin/cost of W hold the linearisation of this xu (the SQP loop), so the base
 // merit comes from them (k_linesearch); otherwise candidate 0 is evaluated.
-int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, double* xu,
-                      const double* sol, const double* goals, int* active, ProblemStats* st, double* alpha_out,
-                      int iter, int mode, bool base_from_lin) {
+// xu: the linearisation point; xu_out: where the updated XU goes (may be xu itself).
+int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
+                      double* xu_out, const double* sol, const double* goals, int* active, ProblemStats* st,
+                      double* alpha_out, int iter, int mode, bool base_from_lin) {
   if (P.B == 0) return I7M_OK;
   const size_t lds = ls_lds_bytes(P.T);
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
   return timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
     if (h->ablate == 4)
-      hipExtLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
     else if (h->spec)
-      hipExtLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
     else
-      hipExtLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, sol, goals, W.fext,
+      hipExtLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
   });
 }
@@ -355,12 +359,11 @@ int chunks_for(const i7m_handle* h, int B) {
   return c;
 }
 
-// The SQP loop on device buffers (xu updated in place).
-int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double* d_goals, int goal_stride,
-            ProblemStats* d_st) {
-  HIPCHK(hipMemsetAsync(d_st, 0, sizeof(ProblemStats) * (size_t)B, h->stream));
-  // all problems start active
-  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->d_active), 1, (size_t)B, h->stream));
+// The SQP loop on device buffers: iteration 1 reads xu_in and its line search writes every
+// row of xu_out; later iterations update xu_out in place (xu_in == xu_out is allowed).  The
+// first linearisation also initialises the active flags and the stats (no memset launches).
+int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const double* d_xs, const double* d_goals,
+            int goal_stride, ProblemStats* d_st) {
   const int C = chunks_for(h, B);
   const long N = h->cfg.N, T = 18 * N - 6;
   hipStream_t ss[I7M_MAX_CHUNKS];
@@ -381,14 +384,19 @@ int run_sqp(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double
       const Bufs W = bufs_at(h, o);
       SolveParams P = params_of(h, b0[c + 1] - b0[c], goal_stride);
       double* xu = d_xu + o * T;
+      const double* xin = (it == 0 ? d_xu_in : d_xu) + o * T;
       const double* xs = d_xs + o * 12;
       const double* g = d_goals + o * N * goal_stride;
       int* act = h->d_active + o;
       int rc;
-      if ((rc = launch_linearize(h, ss[c], W, P, xu, g, act))) return rc;
+      if (it == 0)
+        rc = launch_linearize(h, ss[c], W, P, xin, g, nullptr, act, d_st + o);
+      else
+        rc = launch_linearize(h, ss[c], W, P, xin, g, act);
+      if (rc) return rc;
       const double* qsol = nullptr;
-      if ((rc = solve_qp(h, ss[c], W, P, xu, xs, act, h->d_sol + o * T, &qsol))) return rc;
-      if ((rc = launch_linesearch(h, ss[c], W, P, xu, qsol, g, act, d_st + o, nullptr, it, 0, h->ablate != 6)))
+      if ((rc = solve_qp(h, ss[c], W, P, xin, xs, act, h->d_sol + o * T, &qsol))) return rc;
+      if ((rc = launch_linesearch(h, ss[c], W, P, xin, xu, qsol, g, act, d_st + o, nullptr, it, 0, h->ablate != 6)))
         return rc;
     }
   }
@@ -410,18 +418,19 @@ void drop_graphs(i7m_handle* h) {
 // removes the per-launch host cost and the dispatch gaps (what dominates small-batch latency).
 // A graph is keyed by every argument that reaches a kernel; a miss captures the same launch
 // sequence once.  Timing runs (events) and multi-range runs go direct.
-int run_sqp_graphed(i7m_handle* h, int B, double* d_xu, const double* d_xs, const double* d_goals, int goal_stride,
-                    ProblemStats* d_st) {
-  if (!h->use_graph || h->timing || chunks_for(h, B) > 1) return run_sqp(h, B, d_xu, d_xs, d_goals, goal_stride, d_st);
+int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const double* d_xs, const double* d_goals,
+                    int goal_stride, ProblemStats* d_st) {
+  if (!h->use_graph || h->timing || chunks_for(h, B) > 1)
+    return run_sqp(h, B, d_xu_in, d_xu, d_xs, d_goals, goal_stride, d_st);
   const int hf = h->has_fext ? 1 : 0;
   i7m_handle::GraphEntry* hit = nullptr;
   for (auto& g : h->graphs)
-    if (g.B == B && g.goal_stride == goal_stride && g.has_fext == hf && g.xu == d_xu && g.xs == d_xs &&
+    if (g.B == B && g.goal_stride == goal_stride && g.has_fext == hf && g.xu_in == d_xu_in && g.xu == d_xu && g.xs == d_xs &&
         g.goals == d_goals && g.st == d_st && g.stream == (const void*)h->stream)
       hit = &g;
   if (!hit) {
     HIPCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    const int rc = run_sqp(h, B, d_xu, d_xs, d_goals, goal_stride, d_st);
+    const int rc = run_sqp(h, B, d_xu_in, d_xu, d_xs, d_goals, goal_stride, d_st);
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(h->stream, &graph);
     if (rc) {
@@ -440,7 +449,7 @@ int run_sqp_graphed(i7m_handle* h, int B, double* d_xu, const double* d_xs, cons
       hipGraphExecDestroy(h->graphs[lru].exec);
       h->graphs.erase(h->graphs.begin() + lru);
     }
-    h->graphs.push_back({B, goal_stride, hf, d_xu, d_xs, d_goals, d_st, (const void*)h->stream, exec, 0});
+    h->graphs.push_back({B, goal_stride, hf, d_xu_in, d_xu, d_xs, d_goals, d_st, (const void*)h->stream, exec, 0});
     hit = &h->graphs.back();
   }
   hit->last_use = ++h->graph_clock;
@@ -643,11 +652,8 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (B == 0) return I7M_OK;
   if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
   HIPCHK(hipSetDevice(h->dev));
-  const size_t T = 18 * (size_t)h->cfg.N - 6;
-  if (d_xu_out != d_xu_in)
-    HIPCHK(hipMemcpyAsync(d_xu_out, d_xu_in, (size_t)B * T * 8, hipMemcpyDeviceToDevice, h->stream));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
-  return run_sqp_graphed(h, B, d_xu_out, d_xcur, d_goals, goal_stride, st);
+  return run_sqp_graphed(h, B, d_xu_in, d_xu_out, d_xcur, d_goals, goal_stride, st);
 }
 
 int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,
@@ -661,7 +667,7 @@ int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur,
   if ((rc = copy_in(h, h->d_xu, xu_in, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = run_sqp_graphed(h, B, h->d_xu, h->d_xs, h->d_goal, goal_stride, h->d_stats))) return rc;
+  if ((rc = run_sqp_graphed(h, B, h->d_xu, h->d_xu, h->d_xs, h->d_goal, goal_stride, h->d_stats))) return rc;
   if ((rc = copy_out(h, xu_out, h->d_xu, (size_t)B * T))) return rc;
   if (stats)
     HIPCHK(hipMemcpyAsync(stats, h->d_stats, sizeof(ProblemStats) * (size_t)B, hipMemcpyDeviceToHost, h->stream));
@@ -755,7 +761,7 @@ int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_sol, xu_full, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
-  if ((rc = launch_linesearch(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1,
+  if ((rc = launch_linesearch(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xu, h->d_sol, h->d_goal, nullptr, h->d_stats, h->d_out, 0, 1,
                              false))) return rc;
   if ((rc = copy_out(h, alpha, h->d_out, (size_t)B))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));

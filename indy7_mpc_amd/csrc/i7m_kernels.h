@@ -184,7 +184,7 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
 
 template <bool SPEC, int ABL = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
-                                                   double* __restrict__ xu, const double* __restrict__ sol,
+                                                   const double* xu, double* xu_out, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
                                                    int* __restrict__ active,
                                                    ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
@@ -199,7 +199,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int slot = l / N;
   const int k = l - slot * N;
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
-  double* X = xu + (long)b * P.T;
+  const double* X = xu + (long)b * P.T;
+  double* XO = xu_out + (long)b * P.T;  // the updated XU (may be X itself)
   const double* S = sol + (long)b * P.T;
   // the problem's XU and QP minimiser, staged once in LDS for every round
   // dynamic LDS (ls_lds_bytes): (XU, sol - XU) pairs (T) | RNEA link-force parking (rnea NLDS), which
@@ -331,6 +332,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       st->qp_iters = P.max_iters;
       active[b] = 0;
     }
+    if (XO != X)
+      for (int e = l; e < P.T; e += 64) XO[e] = sXD[e].x;
     return;
   }
   double ss = 0.0;
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const XD p = sXD[e];
     const double xv = p.x;
     const double stp = alpha * p.d;
-    X[e] = xv + stp;
+    XO[e] = xv + stp;
     ss += stp * stp;
   }
   // wave reduction

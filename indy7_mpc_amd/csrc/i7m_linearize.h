@@ -66,7 +66,8 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
                                                   const double* __restrict__ xu, const double* __restrict__ goals,
                                                   const double* __restrict__ fext, const int* __restrict__ active,
                                                   double* __restrict__ lin, double* __restrict__ cost,
-                                                  double* __restrict__ qpd = nullptr) {
+                                                  double* __restrict__ qpd = nullptr, int* __restrict__ init_active = nullptr,
+                                                  ProblemStats* __restrict__ init_stats = nullptr) {
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   const int l = threadIdx.x;
   const int g = l / 6;
@@ -75,6 +76,13 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
   const int b = (int)(kg / P.N);
   const int k = (int)(kg - (long)b * P.N);
   const bool valid = (g < KPW) && (b < P.B) && (!active || active[b]);
+  // first SQP iteration: every problem starts active with zeroed stats (knot 0's lanes)
+  if (init_active && g < KPW && b < P.B && k == 0) {
+    if (j == 0) init_active[b] = 1;
+    double* z = reinterpret_cast<double*>(init_stats + b);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) z[3 * j + r] = 0.0;
+  }
   const bool dyn = valid && (k < P.N - 1);
   const int gg = g < KPW ? g : 0;
 

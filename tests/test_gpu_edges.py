@@ -91,3 +91,34 @@ def test_mixed_batch_extremes(lib, model):
     out, st = h.solve(xcur, goals, XU)
     assert np.isfinite(out).all()
     _check_sqp(out, st, xcur, goals, XU, N=N)
+
+
+def test_device_solve_out_of_place(lib, model):
+    """i7m_solve_device with xu_out != xu_in: the input is only read, every output row is
+    written (including a row whose line search fails: problem 5 has NaN goals, so it must come
+    back unchanged and leave its neighbours alone), and the result equals the in-place
+    host-path solve; a second call on the same buffers gives the same answer (no state leaks
+    through the in-kernel initialisation of the active flags and stats)."""
+    import torch
+
+    N, B = 32, 37
+    xcur, goals, XU = synthetic_batch(B, N, seed=77)
+    goals[5] = np.nan  # a poisoned problem: every merit is NaN, so no alpha is accepted
+    h = lib.Handle(model, N=N, max_batch=B)
+    ref, st_ref = h.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(ref[5], XU[5])  # returned unchanged (src/osqp_sqp.py:81-82)
+    assert st_ref["alphas"][5][0] == 0.0
+    others = np.arange(B) != 5
+    assert np.isfinite(ref[others]).all()
+    dev = torch.device("cuda", 0)
+    t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
+    t_out = torch.full_like(t_xu, float("nan"))
+    t_st = torch.zeros(B * lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
+        torch.cuda.synchronize(dev)
+        np.testing.assert_array_equal(t_out.cpu().numpy(), ref)
+        np.testing.assert_array_equal(t_xu.cpu().numpy(), XU)
+        st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=lib.STATS_DTYPE)
+        np.testing.assert_array_equal(st["qp_iters"], st_ref["qp_iters"])
+        np.testing.assert_array_equal(st["alphas"], st_ref["alphas"])
