@@ -89,6 +89,7 @@ struct i7m_handle {
   bool use_graph = true;  // I7M_GRAPH=0 disables
   // concurrent problem ranges (run_sqp): worker streams + fork/join events
   int chunks = 0;  // 0: automatic (chunks_for), else I7M_CHUNKS
+  int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
   hipStream_t workers[I7M_MAX_CHUNKS] = {};
   hipEvent_t fork = nullptr, join[I7M_MAX_CHUNKS] = {};
   // timing
@@ -271,11 +272,19 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
                       double* xu_out, const double* sol, const double* goals, int* active, ProblemStats* st,
                       double* alpha_out, int iter, int mode, bool base_from_lin) {
   if (P.B == 0) return I7M_OK;
-  const size_t lds = ls_lds_bytes(P.T);
+  // small batches leave most SIMDs idle: spend them on evaluating every candidate in one round
+  const int nw = h->ls_waves > 0 ? h->ls_waves : (P.B <= 256 ? 4 : 1);
+  const size_t lds = ls_lds_bytes(P.T, nw);
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
   return timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
-    if (h->ablate == 4)
+    if (nw == 4 && h->spec)
+      hipExtLaunchKernelGGL((k_linesearch<true, 0, 4>), dim3(P.B), dim3(256), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol,
+                            goals, W.fext, active, st, alpha_out, iter, mode, ln, cs);
+    else if (nw == 4)
+      hipExtLaunchKernelGGL((k_linesearch<false, 0, 4>), dim3(P.B), dim3(256), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol,
+                            goals, W.fext, active, st, alpha_out, iter, mode, ln, cs);
+    else if (h->ablate == 4)
       hipExtLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
                          active, st, alpha_out, iter, mode, ln, cs);
     else if (h->spec)
@@ -549,6 +558,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_IPM"))
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
+  if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c)
     if (hipStreamCreateWithFlags(&h->workers[c], hipStreamNonBlocking) != hipSuccess ||

@@ -114,11 +114,10 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // waves per CU.  Measured 151 -> 132 us (1 wave/SIMD before); staging matters more than the
 // ~90 B/lane of spill the 2-wave target leaves.
 constexpr int LS_NLDS = 3;  // links whose RNEA forces k_linesearch parks in LDS
-// dynamic LDS of k_linesearch for trajectory length T
-inline size_t ls_lds_bytes(int T) {
-  const int park = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
-  return sizeof(double) * (size_t)(2 * T + park);
-}
+// per-wave LDS parking of k_linesearch (RNEA forces; the non-power-of-2 reduction reuses it)
+constexpr int LS_PARK = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
+// dynamic LDS of k_linesearch for trajectory length T and W waves per problem
+inline size_t ls_lds_bytes(int T, int W = 1) { return sizeof(double) * (size_t)(2 * T + W * LS_PARK); }
 // A trajectory entry staged for the line search: XU and the QP step sol - XU side by side, so
 // a line-search point x + al d is one 16-byte LDS read.
 struct alignas(16) XD {
@@ -182,8 +181,11 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
   }
 }
 
-template <bool SPEC, int ABL = 0>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
+// W waves per problem (small batches, where the GPU is otherwise idle): wave w evaluates the
+// candidate slots c0 + w R .. c0 + w R + R - 1 of each round, so W R candidates per round (all
+// eight alphas in one round at N = 32, W = 4).  Same first-accept rule, same merits.
+template <bool SPEC, int ABL = 0, int W = 1>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    const double* xu, double* xu_out, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
                                                    int* __restrict__ active,
@@ -193,7 +195,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
-  const int l = threadIdx.x;
+  const int l = threadIdx.x & 63;
+  const int w = W > 1 ? (int)(threadIdx.x >> 6) : 0;
   const int N = P.N;
   const int R = (N >= 64) ? 1 : 64 / N;
   const int slot = l / N;
@@ -207,11 +210,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // also holds the non-power-of-2 reduction (a different phase of each round)
   extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
   XD* sXD = reinterpret_cast<XD*>(ls_dyn);
-  double* fpark = ls_dyn + 2 * P.T;
+  double* fpark = ls_dyn + 2 * P.T + w * LS_PARK;
   double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
   __shared__ double merit[9];
   {
-    for (int e = l; e < P.T; e += 64) {
+    for (int e = threadIdx.x; e < P.T; e += 64 * W) {
       const double xv = X[e];
       sXD[e] = XD{xv, S[e] - xv};
     }
@@ -222,17 +225,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const double* f6 = fext ? fext + 6L * b : nullptr;
   lds_sync();
   // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
-  auto reduce_store = [&](double o[4], int c0) {
+  // (c0 already offset by this wave's share of the round; `store` false: compute only)
+  auto reduce_store = [&](double o[4], int c0, bool store) {
     if (pow2) {
       // tree-sum the N knots of each candidate slot with shuffles (segments of width N)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         for (int off = N >> 1; off >= 1; off >>= 1) o[j] += __shfl_xor(o[j], off, 64);
-      if (k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
+      if (store && k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
     } else {
       part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
       lds_sync();
-      if (l < R && c0 + l < 1 + NALPHA) {
+      if (store && l < R && c0 + l < 1 + NALPHA) {
         double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
         for (int kk = 0; kk < N; ++kk) {
           qc += part[l * N + kk][0];
@@ -274,13 +278,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         o[3] = sqrt(eq) + sqrt(ev);
       }
     }
-    reduce_store(o, 0);
+    reduce_store(o, 0, w == 0);
     cstart = 1;
   }
   double base = 0.0;
   int found = -1;
-  for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R) {
-    const int cand = c0 + slot;
+  for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R * W) {
+    const int cw = c0 + w * R;  // this wave's first candidate of the round
+    const int cand = cw + slot;
     double o[4] = {0.0, 0.0, 0.0, 0.0};
     if (slot < R && k < N && cand < 1 + NALPHA) {
       // merit terms of (candidate, knot k): the knot values are recomputed from the LDS copy of
@@ -311,13 +316,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         o[3] += sqrt(dd);
       }
     }
-    reduce_store(o, c0);
+    reduce_store(o, cw, true);
     base = merit[0];
-    for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R && cc < 1 + NALPHA; ++cc) {
+    for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R * W && cc < 1 + NALPHA; ++cc) {
       if (merit[cc] <= base) { found = cc; break; }
     }
     lds_sync();
   }
+  if (W > 1 && w != 0) return;  // one wave applies the step
   const double alpha = (found > 0) ? alphas[found - 1] : 0.0;
   if (mode == 1) {
     if (l == 0) alpha_out[b] = alpha;

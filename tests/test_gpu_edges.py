@@ -122,3 +122,22 @@ def test_device_solve_out_of_place(lib, model):
         st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=lib.STATS_DTYPE)
         np.testing.assert_array_equal(st["qp_iters"], st_ref["qp_iters"])
         np.testing.assert_array_equal(st["alphas"], st_ref["alphas"])
+
+
+@pytest.mark.parametrize("N", [32, 20, 64])
+def test_linesearch_one_and_four_waves_agree(lib, model, N, monkeypatch):
+    """k_linesearch with one wave per problem (the B > 256 path) and with four (the small-batch
+    path: all candidates of a round spread over four waves) computes the same merits and the
+    same first-accept alpha, so whole solves are bit-identical; N = 20 takes the non-power-of-2
+    reduction, N = 64 one candidate per wave."""
+    B = 9
+    xcur, goals, XU = synthetic_batch(B, N, seed=300 + N)
+    outs = []
+    for nw in ("1", "4"):
+        monkeypatch.setenv("I7M_LS_WAVES", nw)
+        h = lib.Handle(model, N=N, max_batch=B)
+        outs.append(h.solve(xcur, goals, XU))
+        h.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1]["alphas"], outs[1][1]["alphas"])
+    _check_sqp(outs[1][0], outs[1][1], xcur, goals, XU, N=N)
