@@ -18,7 +18,7 @@ import threading
 import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libindy7mpc.so")
+LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8

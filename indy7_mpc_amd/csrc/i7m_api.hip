@@ -237,31 +237,33 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
   });
 }
 
+template <int ABL>
+void launch_riccati_mfma(hipStream_t s, hipEvent_t ea, hipEvent_t eb, const Bufs& W, const SolveParams& P,
+                         const double* xu, const double* xs, const int* active, double* sol) {
+  hipExtLaunchKernelGGL(k_riccati_mfma<ABL>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active,
+                        W.kbuf, sol, (const double*)nullptr, (const double*)nullptr);
+}
+
 int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
                    const double* xs, const int* active, double* sol) {
   if (P.B == 0) return I7M_OK;
   return timed(h, s, I7M_K_RICCATI, [&](hipEvent_t ea, hipEvent_t eb) {
-    if (h->ric_impl == 1)
+    if (h->ric_impl == 1) {
       hipExtLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
-                         W.kbuf, sol);
-    else if (h->ablate == 1)
-      hipExtLaunchKernelGGL(k_riccati_mfma<1>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
-    else if (h->ablate == 10)
-      hipExtLaunchKernelGGL(k_riccati_mfma<8>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
-    else if (h->ablate == 11)
-      hipExtLaunchKernelGGL(k_riccati_mfma<24>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
-    else if (h->ablate == 8)
-      hipExtLaunchKernelGGL(k_riccati_mfma<4>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
-    else if (h->ablate == 2)
-      hipExtLaunchKernelGGL(k_riccati_mfma<2>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
-    else
-      hipExtLaunchKernelGGL(k_riccati_mfma<0>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                         sol, (const double*)nullptr, (const double*)nullptr);
+                            W.kbuf, sol);
+      return;
+    }
+    // I7M_ABLATE -> ABL bits of riccati_mfma_body (diagnostic timing builds, results invalid)
+    switch (h->ablate) {
+      case 1: launch_riccati_mfma<1>(s, ea, eb, W, P, xu, xs, active, sol); break;      // no rollout
+      case 2: launch_riccati_mfma<6>(s, ea, eb, W, P, xu, xs, active, sol); break;      // scaling for GJ
+      case 8: launch_riccati_mfma<4>(s, ea, eb, W, P, xu, xs, active, sol); break;      // LDS-exchange GJ
+      case 10: launch_riccati_mfma<8>(s, ea, eb, W, P, xu, xs, active, sol); break;     // kbuf slot 0
+      case 11: launch_riccati_mfma<24>(s, ea, eb, W, P, xu, xs, active, sol); break;    // + lin slot 0
+      case 13: launch_riccati_mfma<32>(s, ea, eb, W, P, xu, xs, active, sol); break;    // rollout dead
+      case 18: launch_riccati_mfma<448>(s, ea, eb, W, P, xu, xs, active, sol); break;   // rollout chain only
+      default: launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
+    }
   });
 }
 

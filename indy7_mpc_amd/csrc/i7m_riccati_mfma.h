@@ -16,6 +16,10 @@
 //     A[row=l&15][k=l>>4], B[k=l>>4][col=l&15], D[row=(l>>4)+4i][col=l&15], i=0..3.
 #pragma once
 
+#ifndef I7M_RIC_FD
+#define I7M_RIC_FD 2  // forward-rollout prefetch depth (stages)
+#endif
+
 #include "i7m_kernels.h"
 #include "i7m_riccati.h"
 
@@ -73,10 +77,13 @@ __device__ __forceinline__ double rcp_nr(double d) {
   return y * (2.0 - d * y);
 }
 
-// ABL (diagnostic builds only, results invalid): bit 0 skips the forward rollout, bit 1
-// replaces the Gauss-Jordan solve by a scaling, bit 3 sends every stage's kbuf traffic to stage
-// 0's slot (cache-resident), bit 4 the rollout's lin re-reads likewise; used to split the
-// kernel's time.
+// ABL (diagnostic builds only, results invalid; I7M_ABLATE in i7m_api.hip maps onto them):
+// bit 0 skips the forward rollout, bit 2 selects the LDS-exchange Gauss-Jordan (bit 1 then
+// replaces it by a scaling), bit 3 sends every stage's kbuf traffic to stage 0's slot
+// (cache-resident), bit 4 the rollout's lin re-reads likewise, bit 5 drops the rollout's
+// stores (the compiler then drops the rollout's arithmetic), bit 6 feeds x instead of u to the
+// rollout's B u term (shorter chain), bit 7 skips the rollout's LDS staging, bit 8 keeps only
+// the last stage's stores; used to split the kernel's time.
 // BOX: the interior-point Newton step of the box-constrained QP (oracle/box_ipm.py): the same
 // QP with Hessian P + diag(Sigma) and linear term g + h, Sigma and h given per variable in
 // bsig / bh (B, T).  The equality rows are unchanged, so the result is the Newton iterate
@@ -242,7 +249,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     d4 Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
     double* kk = KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE;
-    if (!(ABL & 4) && !BOX) {
+    if ((ABL & 4) && !BOX) {
+      // (Diagnostic alternative, I7M_ABLATE=8: measured 5 us slower per launch at B = 1 and
+      // level at B = 4096 than the column-per-lane elimination below)
       // K~ = -H^-1 G~ by Gauss-Jordan on [H | G~] (6 x 19) in place in the MFMA accumulator
       // layout: lane l holds column lr of rows lq and lq + 4 (lq < 2) of H (lr < 6) and of G~
       // (lr < 13).  Pivot p needs, per lane, M[r][p] of its two rows (published by the lanes
@@ -291,8 +300,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       if (l < 6) kk[78 + l] = sh[MO_CV + l];
     } else {
-      // Column-per-lane Gauss-Jordan with v_readlane pivot broadcast (the box variants; for the
-      // plain QP a diagnostic A/B, I7M_ABLATE=8): H, G~ through LDS, one column of [H | G~] per
+      // Column-per-lane Gauss-Jordan with v_readlane pivot broadcast (every variant by default):
+      // H, G~ through LDS, one column of [H | G~] per
       // lane (lanes 0..18); HINV adds the identity columns in lanes 19..24, which end as H^-1.
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -339,19 +348,27 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
   // Lane l < 12 holds x_l and lane m < 6 holds u_m; every lane sees the full vectors through
   // v_readlane.  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
-  // (3 per lane) FD stages ahead into registers and dropped into one LDS slot permuted so that
+  // (3 per lane) two stages ahead into registers and dropped into one LDS slot permuted so that
   // the 19 values each lane needs are contiguous: lane m < 6 the row m of K~ (13, then zeros),
   // lane 6 + i c_v[i] and row i of Aq, Av, Bu; lanes >= 12 an all-zero block.  Every lane then
   // reads its block with the same ds_read_b128 sequence (no divergent gathers).
   if (ABL & 1) return;
-  constexpr int FD = 2;
   constexpr int FB = 20;  // doubles per lane block
   __syncthreads();  // kbuf stores of the backward sweep -> loads below (same workgroup)
   double* S = sol + (long)b * P.T;
-  auto fsrc = [&](int k, int e) -> const double* {
-    return (e < KBUF_STRIDE) ? KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE + e
-                             : LINb + (long)((ABL & 16) ? 0 : k) * LIN_STRIDE + (e - KBUF_STRIDE);
+  // stage element e of stage k lives at base + k * stride (resolved once per lane)
+  auto fbase = [&](int e, int& stride) -> const double* {
+    if (e < KBUF_STRIDE) {
+      stride = (ABL & 8) ? 0 : KBUF_STRIDE;
+      return KB + e;
+    }
+    stride = (ABL & 16) ? 0 : LIN_STRIDE;
+    return LINb + (e - KBUF_STRIDE);
   };
+  int fs0, fs1, fs2;
+  const double* fb0 = fbase(l, fs0);
+  const double* fb1 = fbase(l + 64, fs1);
+  const double* fb2 = fbase(l + 128, fs2);
   // slot position of stage element e
   auto fpos = [](int e) -> int {
     if (e < 78) return FB * (e / 13) + e % 13;
@@ -363,35 +380,39 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   double* myb = sh + FB * (l < 12 ? l : 12);
   // zero the slot once (K~ rows' tails and the spare block stay zero)
   for (int e = l; e < FB * 13; e += 64) sh[e] = 0.0;
+  // FD prefetch buffers used in turn (the loop is unrolled by FD), each refilled FD stages
+  // ahead right after it is dropped into LDS: no register rotation, whose copies made every
+  // stage wait for the loads it had just issued.
+  constexpr int FD = I7M_RIC_FD;
   double f[FD][3];
-#pragma unroll
-  for (int d = 0; d < FD; ++d) {
-    const int kk = (d < N - 1) ? d : 0;
-    f[d][0] = *fsrc(kk, l);
-    f[d][1] = *fsrc(kk, l + 64);
-    f[d][2] = *fsrc(kk, l + 128);
-  }
+  auto fload = [&](double* f, int kk) {
+    f[0] = fb0[(long)kk * fs0];
+    f[1] = fb1[(long)kk * fs1];
+    f[2] = fb2[(long)kk * fs2];
+  };
   double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
   if (l < 12) S[l] = xreg;
-  for (int k = 0; k < N - 1; ++k) {
-    lds_sync();
-    sh[w0] = f[0][0];
-    sh[w1] = f[0][1];
-    sh[w2] = f[0][2];
+  // drain x_0 before the prefetch: otherwise the waitcnt pass carries the (lane-conditional)
+  // x_0 load into the loop and every stage waits for the loads it has just issued
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
-    for (int d = 0; d + 1 < FD; ++d) {
-      f[d][0] = f[d + 1][0];
-      f[d][1] = f[d + 1][1];
-      f[d][2] = f[d + 1][2];
-    }
-    const int kn = (k + FD < N - 1) ? k + FD : k;
-    f[FD - 1][0] = *fsrc(kn, l);
-    f[FD - 1][1] = *fsrc(kn, l + 64);
-    f[FD - 1][2] = *fsrc(kn, l + 128);
-    lds_sync();
+  for (int d = 0; d < FD; ++d) fload(f[d], d < N - 1 ? d : 0);
+  auto stage = [&](const int k, double* fk) {
     double r[19];
+    if (ABL & 128) {
+#pragma unroll
+      for (int j = 0; j < 19; ++j) r[j] = fk[j % 3] * (j + 1);
+      fload(fk, (k + FD < N - 1) ? k + FD : k);
+    } else {
+    lds_sync();
+    sh[w0] = fk[0];
+    sh[w1] = fk[1];
+    sh[w2] = fk[2];
+    fload(fk, (k + FD < N - 1) ? k + FD : k);
+    lds_sync();
 #pragma unroll
     for (int j = 0; j < 19; ++j) r[j] = myb[j];
+    }
     double X[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
@@ -400,7 +421,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
     for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
     const double ureg = ua + ub;
-    if (l < 6) S[18 * k + 12 + l] = ureg;
+    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 6) S[18 * k + 12 + l] = ureg;
     double U[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
@@ -409,14 +430,24 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     for (int j = 0; j < 6; ++j) {
       va += r[1 + j] * X[j];
       vb += r[7 + j] * X[6 + j];
-      vc += r[13 + j] * U[j];
+      vc += r[13 + j] * ((ABL & 64) ? X[j] : U[j]);
     }
     // q lanes: q + dt v, v_l = x_{6+l} from lane l + 6 (DPP row shift, same 16-lane row)
     const double vq = row_shl6_f64(xreg);
     const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
     xreg = nx;
-    if (l < 12) S[18 * (k + 1) + l] = nx;
+    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 12) S[18 * (k + 1) + l] = nx;
+  };
+  // all FD stages unconditional inside the loop (the tail after it): a path that skips a stage
+  // and loops back would make the next stage wait for its own refill
+  int k = 0;
+  for (; k + FD - 1 < N - 1; k += FD) {
+#pragma unroll
+    for (int d = 0; d < FD; ++d) stage(k + d, f[d]);
   }
+#pragma unroll
+  for (int d = 0; d < FD - 1; ++d)
+    if (k + d < N - 1) stage(k + d, f[d]);
 }
 
 // The corrector Newton step of I7M_QP_BOX (k_ipm_fused): the QP of the last
@@ -484,7 +515,6 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   }
   // forward: as the main rollout (stage slot K~ 78 | c_v 6 | Aq Av Bu 108), c = 0, x_0 = 0, and
   // the result added to y by the lanes that wrote y's entries
-  constexpr int FD = 2;
   __syncthreads();  // kff stores -> loads below
   double* Y = y + (long)b * P.T;
   const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
@@ -492,30 +522,22 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   auto fsrc = [&](int k, int e) -> const double* {
     return (e < KBUF_STRIDE) ? KB + (long)k * KBUF_STRIDE + e : LINb + (long)k * LIN_STRIDE + (e - KBUF_STRIDE);
   };
-  double f[FD][3];
-#pragma unroll
-  for (int d = 0; d < FD; ++d) {
-    const int kk = (d < N - 1) ? d : 0;
-    f[d][0] = *fsrc(kk, l);
-    f[d][1] = *fsrc(kk, l + 64);
-    f[d][2] = *fsrc(kk, l + 128);
-  }
+  // two alternating prefetch buffers, as the main rollout
+  double fa[3], fb[3];
+  auto fload = [&](double* f, int kk) {
+    f[0] = *fsrc(kk, l);
+    f[1] = *fsrc(kk, l + 64);
+    f[2] = *fsrc(kk, l + 128);
+  };
+  fload(fa, 0);
+  fload(fb, N - 1 > 1 ? 1 : 0);
   double xreg = 0.0;
-  for (int k = 0; k < N - 1; ++k) {
+  auto stage = [&](const int k, double* f) {
     lds_sync();
-    sh[l] = f[0][0];
-    sh[l + 64] = f[0][1];
-    sh[l + 128] = f[0][2];
-#pragma unroll
-    for (int d = 0; d + 1 < FD; ++d) {
-      f[d][0] = f[d + 1][0];
-      f[d][1] = f[d + 1][1];
-      f[d][2] = f[d + 1][2];
-    }
-    const int kn = (k + FD < N - 1) ? k + FD : k;
-    f[FD - 1][0] = *fsrc(kn, l);
-    f[FD - 1][1] = *fsrc(kn, l + 64);
-    f[FD - 1][2] = *fsrc(kn, l + 128);
+    sh[l] = f[0];
+    sh[l + 64] = f[1];
+    sh[l + 128] = f[2];
+    fload(f, (k + 2 < N - 1) ? k + 2 : k);
     lds_sync();
     double r[19];
     if (l < 6) {
@@ -554,7 +576,13 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
     const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
     xreg = nx;
     if (l < 12) Y[18 * (k + 1) + l] += nx;
+  };
+  int k = 0;
+  for (; k + 1 < N - 1; k += 2) {
+    stage(k, fa);
+    stage(k + 1, fb);
   }
+  if (k < N - 1) stage(k, fa);
 }
 
 template <int ABL, bool BOX = false>

@@ -11,7 +11,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(B, N, env, steps=100):
+def run(B, N, env, steps=100, **handle_kw):
     import torch
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.model import default_model
@@ -21,7 +21,7 @@ def run(B, N, env, steps=100):
     os.environ.update(env)
     try:
         model = default_model()
-        h = _lib.Handle(model, N=N, max_batch=B)
+        h = _lib.Handle(model, N=N, max_batch=B, **handle_kw)
     finally:
         for k, v in old.items():
             if v is None:
