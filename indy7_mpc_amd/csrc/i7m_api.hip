@@ -421,7 +421,7 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
 }
 
 void drop_graphs(i7m_handle* h) {
-  for (auto& g : h->graphs) hipGraphExecDestroy(g.exec);
+  for (auto& g : h->graphs) (void)hipGraphExecDestroy(g.exec);
   h->graphs.clear();
 }
 
@@ -445,19 +445,19 @@ int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, c
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(h->stream, &graph);
     if (rc) {
-      if (graph) hipGraphDestroy(graph);
+      if (graph) (void)hipGraphDestroy(graph);
       return rc;
     }
     if (e != hipSuccess) return fail(I7M_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
     hipGraphExec_t exec = nullptr;
     const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    hipGraphDestroy(graph);
+    (void)hipGraphDestroy(graph);
     if (ei != hipSuccess) return fail(I7M_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
     if (h->graphs.size() >= 4) {  // evict the least recently used
       size_t lru = 0;
       for (size_t i = 1; i < h->graphs.size(); ++i)
         if (h->graphs[i].last_use < h->graphs[lru].last_use) lru = i;
-      hipGraphExecDestroy(h->graphs[lru].exec);
+      (void)hipGraphExecDestroy(h->graphs[lru].exec);
       h->graphs.erase(h->graphs.begin() + lru);
     }
     h->graphs.push_back({B, goal_stride, hf, d_xu_in, d_xu, d_xs, d_goals, d_st, (const void*)h->stream, exec, 0});
@@ -604,29 +604,29 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
 
 void i7m_destroy(i7m_handle* h) {
   if (!h) return;
-  hipSetDevice(h->dev);
-  if (h->stream) hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->dev);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
                   h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc, h->d_qpd,
                   h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact,
                   h->d_bhinv, h->d_bdh};
   for (void* p : bufs)
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
   for (auto& t : h->ev) {
-    hipEventDestroy(t.a);
-    hipEventDestroy(t.b);
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
   }
-  for (auto e : h->pool) hipEventDestroy(e);
+  for (auto e : h->pool) (void)hipEventDestroy(e);
   drop_graphs(h);
   for (int c = 0; c < I7M_MAX_CHUNKS; ++c) {
     if (h->workers[c]) {
-      hipStreamSynchronize(h->workers[c]);
-      hipStreamDestroy(h->workers[c]);
+      (void)hipStreamSynchronize(h->workers[c]);
+      (void)hipStreamDestroy(h->workers[c]);
     }
-    if (h->join[c]) hipEventDestroy(h->join[c]);
+    if (h->join[c]) (void)hipEventDestroy(h->join[c]);
   }
-  if (h->fork) hipEventDestroy(h->fork);
-  if (h->own) hipStreamDestroy(h->own);
+  if (h->fork) (void)hipEventDestroy(h->fork);
+  if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
 
