@@ -86,7 +86,8 @@ struct i7m_handle {
   };
   std::vector<GraphEntry> graphs;
   unsigned long long graph_clock = 0;
-  bool use_graph = true;  // I7M_GRAPH=0 disables
+  bool use_graph = false;  // I7M_GRAPH=1: capture the solve once per buffer set, replay it
+                           // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
   // concurrent problem ranges (run_sqp): worker streams + fork/join events
   int chunks = 0;  // 0: automatic (chunks_for), else I7M_CHUNKS
   int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)

@@ -93,19 +93,25 @@ def test_mixed_batch_extremes(lib, model):
     _check_sqp(out, st, xcur, goals, XU, N=N)
 
 
-def test_device_solve_out_of_place(lib, model):
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_device_solve_out_of_place(lib, model, graph, monkeypatch):
     """i7m_solve_device with xu_out != xu_in: the input is only read, every output row is
     written (including a row whose line search fails: problem 5 has NaN goals, so it must come
     back unchanged and leave its neighbours alone), and the result equals the in-place
     host-path solve; a second call on the same buffers gives the same answer (no state leaks
-    through the in-kernel initialisation of the active flags and stats)."""
+    through the in-kernel initialisation of the active flags and stats).  graph = "1": the
+    solve captured once into a hipGraph and replayed (I7M_GRAPH=1), against direct launches."""
     import torch
 
     N, B = 32, 37
     xcur, goals, XU = synthetic_batch(B, N, seed=77)
     goals[5] = np.nan  # a poisoned problem: every merit is NaN, so no alpha is accepted
+    monkeypatch.setenv("I7M_GRAPH", "0")
+    h0 = lib.Handle(model, N=N, max_batch=B)
+    ref, st_ref = h0.solve(xcur, goals, XU)
+    h0.close()
+    monkeypatch.setenv("I7M_GRAPH", graph)
     h = lib.Handle(model, N=N, max_batch=B)
-    ref, st_ref = h.solve(xcur, goals, XU)
     np.testing.assert_array_equal(ref[5], XU[5])  # returned unchanged (src/osqp_sqp.py:81-82)
     assert st_ref["alphas"][5][0] == 0.0
     others = np.arange(B) != 5
@@ -114,7 +120,7 @@ def test_device_solve_out_of_place(lib, model):
     t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
     t_out = torch.full_like(t_xu, float("nan"))
     t_st = torch.zeros(B * lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    for _ in range(2):
+    for _ in range(3):
         h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
         torch.cuda.synchronize(dev)
         np.testing.assert_array_equal(t_out.cpu().numpy(), ref)

@@ -1,6 +1,6 @@
 """Small-batch latency A/B (config 2 shape): per-step time and per-kernel launch durations of
 the solve at B in {1, 64, 256} for the default kernels and the variants selected by environment
-knobs read at handle creation (I7M_RICCATI=valu, I7M_GRAPH=0).
+knobs read at handle creation (I7M_RICCATI=valu, I7M_GRAPH=1).
 python tools/small_batch_ab.py"""
 import json
 import os
@@ -62,7 +62,7 @@ def run(B, N, env, steps=100, **handle_kw):
 def main():
     out = []
     for B in (1, 64, 256):
-        for env in ({}, {"I7M_RICCATI": "valu"}, {"I7M_GRAPH": "0"}):
+        for env in ({}, {"I7M_RICCATI": "valu"}, {"I7M_GRAPH": "1"}):
             r = run(B, 32, env)
             out.append(r)
             print(json.dumps(r), flush=True)
