@@ -33,22 +33,41 @@ struct IpmState {
 
 // Bounds of trajectory entry e (knot e / 18, slot e % 18); false if unbounded.  The initial
 // state is fixed by the equality rows and never bounded (oracle/box_ipm.py::box_bounds).
-__device__ __forceinline__ bool box_of(const DevModel& M, int mask, int e, double& lo, double& hi) {
-  const int k = e / 18, j = e - 18 * (e / 18);
-  if (k == 0 && j < 12) return false;
-  if (j < 6) {
-    if (!(mask & 1)) return false;
-    lo = M.qlo[j];
-    hi = M.qhi[j];
-  } else if (j < 12) {
-    if (!(mask & 2)) return false;
-    hi = M.vlim[j - 6];
-    lo = -hi;
-  } else {
-    if (!(mask & 4)) return false;
-    hi = M.ulim[j - 12];
-    lo = -hi;
+// The per-slot bounds of the mask are staged once per kernel in LDS (BoxTab), so the element
+// passes below read them there instead of from the model in global memory.
+struct BoxTab {
+  double lo[18], hi[18];
+  int on[18];
+};
+__device__ __forceinline__ void box_tab_fill(const DevModel& M, int mask, BoxTab* t) {
+  const int j = threadIdx.x;
+  if (j < 18) {
+    double lo = 0.0, hi = 0.0;
+    int on = 0;
+    if (j < 6) {
+      on = mask & 1;
+      lo = M.qlo[j];
+      hi = M.qhi[j];
+    } else if (j < 12) {
+      on = mask & 2;
+      hi = M.vlim[j - 6];
+      lo = -hi;
+    } else {
+      on = mask & 4;
+      hi = M.ulim[j - 12];
+      lo = -hi;
+    }
+    t->lo[j] = lo;
+    t->hi[j] = hi;
+    t->on[j] = on != 0;
   }
+  __syncthreads();
+}
+__device__ __forceinline__ bool box_of(const BoxTab& t, int e, double& lo, double& hi) {
+  const int k = e / 18, j = e - 18 * k;
+  if ((k == 0 && j < 12) || !t.on[j]) return false;
+  lo = t.lo[j];
+  hi = t.hi[j];
   return true;
 }
 
@@ -78,7 +97,7 @@ __device__ __forceinline__ double ratio_min(double t, double v, double dv) {
 // k_ipm_fused runs the whole iteration of one problem in one wave.
 
 // x = clip(x_eq) into the interior, z = 1, mu, and the first predictor's Sigma and h.
-__device__ __forceinline__ IpmState ipm_init_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+__device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveParams& P, const BoxParams& BP, const int b,
                                                   const double* __restrict__ xeq, double* __restrict__ x,
                                                   double* __restrict__ zl, double* __restrict__ zu,
                                                   double* __restrict__ sig, double* __restrict__ h) {
@@ -88,7 +107,7 @@ __device__ __forceinline__ IpmState ipm_init_body(const DevModel& M, const Solve
   int nb = 0;
   for (int e = l; e < P.T; e += 64) {
     double lo, hi, xv = xeq[o + e], z = 0.0, s = 0.0;
-    if (box_of(M, BP.mask, e, lo, hi)) {
+    if (box_of(Bt, e, lo, hi)) {
       const double w = hi - lo;
       xv = fmin(fmax(xv, lo + BP.theta * w), hi - BP.theta * w);
       z = 1.0;
@@ -118,103 +137,189 @@ __device__ __forceinline__ IpmState ipm_init_body(const DevModel& M, const Solve
 
 // Predictor: dx_aff = y - x; affine step lengths and mu_aff; sigma*mu (-> S.smu); the
 // corrector's h.
-__device__ __forceinline__ void ipm_pred_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+// Element passes run in chunks of IPM_U elements per lane: the chunk's operands are all loaded
+// (clamped addresses, no branches) before any is used, so one wave has IPM_U x (2..5) loads in
+// flight instead of waiting out the memory latency element by element.  The per-lane order of
+// every accumulation is unchanged (chunks and their elements in increasing e), so the results
+// are bit-identical to the element-by-element loops.
+#ifndef I7M_IPM_U
+#define I7M_IPM_U 6
+#endif
+constexpr int IPM_U = I7M_IPM_U;
+
+__device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParams& P, const BoxParams& BP, const int b,
                                               const double* __restrict__ y, const double* __restrict__ x,
                                               const double* __restrict__ zl, const double* __restrict__ zu,
                                               double* __restrict__ dxa, double* __restrict__ h, IpmState& S,
                                               double* __restrict__ dh = nullptr) {
   const int l = threadIdx.x;
-  const long o = (long)b * P.T;
+  const int T = P.T;
+  const long o = (long)b * T;
   double ap = 1.0, ad = 1.0;
-  for (int e = l; e < P.T; e += 64) {
-    const double d = y[o + e] - x[o + e];
-    dxa[o + e] = d;
-    double lo, hi;
-    if (box_of(M, BP.mask, e, lo, hi)) {
-      const double xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
-      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
-      ap = ratio_min(ratio_min(ap, sl, d), su, -d);
-      ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
+  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
+    double yv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U];
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = min(e0 + 64 * u, T - 1);
+      yv[u] = y[o + e];
+      xv[u] = x[o + e];
+      av[u] = zl[o + e];
+      cv[u] = zu[o + e];
+    }
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = e0 + 64 * u;
+      if (e < T) {
+        const double d = yv[u] - xv[u];
+        dxa[o + e] = d;
+        double lo, hi;
+        if (box_of(Bt, e, lo, hi)) {
+          const double xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
+          const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+          ap = ratio_min(ratio_min(ap, sl, d), su, -d);
+          ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
+        }
+      }
     }
   }
   ap = wave_min(ap);
   ad = wave_min(ad);
   double acc = 0.0;
-  for (int e = l; e < P.T; e += 64) {
-    double lo, hi;
-    if (box_of(M, BP.mask, e, lo, hi)) {
-      const double d = dxa[o + e], xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
-      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
-      acc += (sl + ap * d) * (a + ad * dzl) + (su - ap * d) * (c + ad * dzu);
+  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
+    double dv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U];
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = min(e0 + 64 * u, T - 1);
+      dv[u] = dxa[o + e];
+      xv[u] = x[o + e];
+      av[u] = zl[o + e];
+      cv[u] = zu[o + e];
+    }
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = e0 + 64 * u;
+      double lo, hi;
+      if (e < T && box_of(Bt, e, lo, hi)) {
+        const double d = dv[u], xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
+        const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+        acc += (sl + ap * d) * (a + ad * dzl) + (su - ap * d) * (c + ad * dzu);
+      }
     }
   }
   acc = wave_sum(acc);
   const double mua = acc / (2.0 * S.nb);
   const double r = mua / S.mu;
   const double smu = r * r * r * S.mu;
-  for (int e = l; e < P.T; e += 64) {
-    double lo, hi, hv = 0.0;
-    if (box_of(M, BP.mask, e, lo, hi)) {
-      const double d = dxa[o + e], xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
-      const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
-      const double rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
-      const double s = a / sl + c / su;
-      hv = -a + c + (rl / sl - ru / su) - s * xv;
+  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
+    double dv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U], hold[IPM_U];
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = min(e0 + 64 * u, T - 1);
+      dv[u] = dxa[o + e];
+      xv[u] = x[o + e];
+      av[u] = zl[o + e];
+      cv[u] = zu[o + e];
+      hold[u] = dh ? h[o + e] : 0.0;
     }
-    if (dh) dh[o + e] = hv - h[o + e];  // the corrector's change of the linear terms
-    h[o + e] = hv;
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = e0 + 64 * u;
+      if (e < T) {
+        double lo, hi, hv = 0.0;
+        if (box_of(Bt, e, lo, hi)) {
+          const double d = dv[u], xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
+          const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+          const double rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
+          const double s = a / sl + c / su;
+          hv = -a + c + (rl / sl - ru / su) - s * xx;
+        }
+        if (dh) dh[o + e] = hv - hold[u];  // the corrector's change of the linear terms
+        h[o + e] = hv;
+      }
+    }
   }
   S.smu = smu;
 }
 
 // Corrector: dx = y - x, common step, update (x, z_l, z_u), new mu, convergence, and the next
 // predictor's Sigma and h.
-__device__ __forceinline__ void ipm_corr_body(const DevModel& M, const SolveParams& P, const BoxParams& BP, const int b,
+__device__ __forceinline__ void ipm_corr_body(const BoxTab& Bt, const SolveParams& P, const BoxParams& BP, const int b,
                                               const double* __restrict__ y, double* __restrict__ x,
                                               double* __restrict__ zl, double* __restrict__ zu,
                                               const double* __restrict__ dxa, double* __restrict__ sig,
                                               double* __restrict__ h, IpmState& S) {
   const int l = threadIdx.x;
-  const long o = (long)b * P.T;
+  const int T = P.T;
+  const long o = (long)b * T;
   const double smu = S.smu;
   double t = 1.0;
-  for (int e = l; e < P.T; e += 64) {
-    double lo, hi;
-    if (box_of(M, BP.mask, e, lo, hi)) {
-      const double d = y[o + e] - x[o + e], da = dxa[o + e];
-      const double xv = x[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
-      const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
-      const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-      const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
-      t = ratio_min(ratio_min(t, sl, d), su, -d);
-      t = ratio_min(ratio_min(t, a, dzl), c, dzu);
+  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
+    double yv[IPM_U], xv[IPM_U], dav[IPM_U], av[IPM_U], cv[IPM_U];
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = min(e0 + 64 * u, T - 1);
+      yv[u] = y[o + e];
+      xv[u] = x[o + e];
+      dav[u] = dxa[o + e];
+      av[u] = zl[o + e];
+      cv[u] = zu[o + e];
+    }
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = e0 + 64 * u;
+      double lo, hi;
+      if (e < T && box_of(Bt, e, lo, hi)) {
+        const double d = yv[u] - xv[u], da = dav[u];
+        const double xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
+        const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+        const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+        const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
+        t = ratio_min(ratio_min(t, sl, d), su, -d);
+        t = ratio_min(ratio_min(t, a, dzl), c, dzu);
+      }
     }
   }
   t = wave_min(t);
   const double al = fmin(1.0, BP.eta * t);
   double acc = 0.0;
-  for (int e = l; e < P.T; e += 64) {
-    const double d = y[o + e] - x[o + e];
-    const double xv = x[o + e];
-    double lo, hi;
-    if (box_of(M, BP.mask, e, lo, hi)) {
-      const double da = dxa[o + e], sl = xv - lo, su = hi - xv, a = zl[o + e], c = zu[o + e];
-      const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
-      const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-      const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
-      const double xn = xv + al * d, an = a + al * dzl, cn = c + al * dzu;
-      x[o + e] = xn;
-      zl[o + e] = an;
-      zu[o + e] = cn;
-      const double sln = xn - lo, sun = hi - xn;
-      acc += sln * an + sun * cn;
-      const double s = an / sln + cn / sun;
-      sig[o + e] = s;
-      h[o + e] = -s * xn;
-    } else {
-      x[o + e] = xv + al * d;
-      sig[o + e] = 0.0;
-      h[o + e] = 0.0;
+  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
+    double yv[IPM_U], xv[IPM_U], dav[IPM_U], av[IPM_U], cv[IPM_U];
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = min(e0 + 64 * u, T - 1);
+      yv[u] = y[o + e];
+      xv[u] = x[o + e];
+      dav[u] = dxa[o + e];
+      av[u] = zl[o + e];
+      cv[u] = zu[o + e];
+    }
+#pragma unroll
+    for (int u = 0; u < IPM_U; ++u) {
+      const int e = e0 + 64 * u;
+      if (e < T) {
+        const double d = yv[u] - xv[u];
+        const double xx = xv[u];
+        double lo, hi;
+        if (box_of(Bt, e, lo, hi)) {
+          const double da = dav[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
+          const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+          const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+          const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
+          const double xn = xx + al * d, an = a + al * dzl, cn = c + al * dzu;
+          x[o + e] = xn;
+          zl[o + e] = an;
+          zu[o + e] = cn;
+          const double sln = xn - lo, sun = hi - xn;
+          acc += sln * an + sun * cn;
+          const double s = an / sln + cn / sun;
+          sig[o + e] = s;
+          h[o + e] = -s * xn;
+        } else {
+          x[o + e] = xx + al * d;
+          sig[o + e] = 0.0;
+          h[o + e] = 0.0;
+        }
+      }
     }
   }
   acc = wave_sum(acc);
@@ -246,7 +351,9 @@ __global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg
                                                  IpmState* __restrict__ st, int* __restrict__ ipm_active) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
-  const IpmState S = ipm_init_body(*Mg, P, BP, b, xeq, x, zl, zu, sig, h);
+  __shared__ BoxTab Bt;
+  box_tab_fill(*Mg, BP.mask, &Bt);
+  const IpmState S = ipm_init_body(Bt, P, BP, b, xeq, x, zl, zu, sig, h);
   if (threadIdx.x == 0) {
     st[b] = S;
     ipm_active[b] = (active ? active[b] : 1) && S.nb > 0;
@@ -260,8 +367,10 @@ __global__ void __launch_bounds__(64) k_ipm_pred(const DevModel* __restrict__ Mg
                                                  IpmState* __restrict__ st, const int* __restrict__ ipm_active) {
   const int b = blockIdx.x;
   if (b >= P.B || !ipm_active[b]) return;
+  __shared__ BoxTab Bt;
+  box_tab_fill(*Mg, BP.mask, &Bt);
   IpmState S = st[b];
-  ipm_pred_body(*Mg, P, BP, b, y, x, zl, zu, dxa, h, S);
+  ipm_pred_body(Bt, P, BP, b, y, x, zl, zu, dxa, h, S);
   if (threadIdx.x == 0) st[b].smu = S.smu;
 }
 
@@ -273,8 +382,10 @@ __global__ void __launch_bounds__(64) k_ipm_corr(const DevModel* __restrict__ Mg
                                                  int* __restrict__ ipm_active) {
   const int b = blockIdx.x;
   if (b >= P.B || !ipm_active[b]) return;
+  __shared__ BoxTab Bt;
+  box_tab_fill(*Mg, BP.mask, &Bt);
   IpmState S = st[b];
-  ipm_corr_body(*Mg, P, BP, b, y, x, zl, zu, dxa, sig, h, S);
+  ipm_corr_body(Bt, P, BP, b, y, x, zl, zu, dxa, sig, h, S);
   if (threadIdx.x == 0) {
     st[b] = S;
     if (ipm_done(S, BP)) ipm_active[b] = 0;
@@ -323,11 +434,13 @@ k_ipm_fused(IpmFusedArgs args) {
   const int b = blockIdx.x;
   if (b >= args.P.B) return;
   __shared__ double sh[MO_TOTAL];
+  __shared__ BoxTab Bt;
   IpmState S;
   bool run;
   {
     const IpmFusedArgs& a = args;
-    S = ipm_init_body(*a.Mg, a.P, a.BP, b, a.xeq, a.x, a.zl, a.zu, a.sig, a.h);
+    box_tab_fill(*a.Mg, a.BP.mask, &Bt);
+    S = ipm_init_body(Bt, a.P, a.BP, b, a.xeq, a.x, a.zl, a.zu, a.sig, a.h);
     ipm_uniform(S);
     run = (a.active ? a.active[b] != 0 : true) && S.nb > 0;
   }
@@ -353,10 +466,10 @@ k_ipm_fused(IpmFusedArgs args) {
     const IpmFusedArgs* B = kernarg_ipm();
     const BoxParams BP = B->BP;
     if (half == 0) {
-      ipm_pred_body(*B->Mg, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
+      ipm_pred_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
       ipm_uniform(S);
     } else {
-      ipm_corr_body(*B->Mg, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->sig, B->h, S);
+      ipm_corr_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->sig, B->h, S);
       ipm_uniform(S);
       run = !ipm_done(S, BP);
     }

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--box", action="store_true", help="config 4: box rows (I7M_QP_BOX), seed 46")
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -26,11 +27,11 @@ def main():
 
     dev = torch.device("cuda", 0)
     model = default_model()
-    h = _lib.Handle(model, N=a.N, max_batch=a.batch)
+    h = _lib.Handle(model, N=a.N, max_batch=a.batch, **({"qp_mode": _lib.QP_BOX} if a.box else {}))
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
     h.set_stream(s.cuda_stream)
-    xcur, goals, XU = make_batch(h, model, a.batch, a.N, seed=45)
+    xcur, goals, XU = make_batch(h, model, a.batch, a.N, seed=46 if a.box else 45)
     t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
     t_out = torch.empty_like(t_xu)
     for _ in range(a.warmup + a.steps):
