@@ -137,9 +137,12 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
                                                       const double* f6, double* fpark, double* o) {
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
   const int ok = 18 * k, on = 18 * (last ? k : k + 1);
+  // both halves of the pair in one 16-byte read and a select (written as `base_pt ? x : x + al d`
+  // the compiler made the d read a branch of its own, serialising every knot value's LDS reads)
   auto val = [&](int e) -> double {
     const XD p = sXD[e];
-    return base_pt ? p.x : p.x + al * p.d;
+    const double v = p.x + al * p.d;
+    return base_pt ? p.x : v;
   };
   double c[6], sn[6], pe[3];
   {
@@ -297,7 +300,8 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
       const int ok = 18 * k, on = 18 * (last ? k : k + 1);
       auto val = [&](int e) -> double {
         const XD p = sXD[e];
-        return base_pt ? p.x : p.x + al * p.d;
+        const double v = p.x + al * p.d;
+        return base_pt ? p.x : v;
       };
       if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
