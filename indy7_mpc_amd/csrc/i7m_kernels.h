@@ -172,13 +172,33 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
     o[2] = P.R * uu;
     forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark);
     asm volatile("" ::: "memory");  // re-read the knot values from LDS below
+    // the knot values in two halves of 12 LDS pair reads, each half issued before its
+    // arithmetic (interleaved with it, the scheduler reused one register set and waited on each
+    // read in turn)
     double eq = 0.0, ev = 0.0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const double dq = (val(ok + i) + val(ok + 6 + i) * P.dt) - val(on + i);
-      const double dv = (val(ok + 6 + i) + a[i] * P.dt) - val(on + 6 + i);
-      eq += dq * dq;
-      ev += dv * dv;
+    for (int hf = 0; hf < 2; ++hf) {
+      XD pq[3], pv[3], pn[3], pw[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pq[i] = sXD[ok + 3 * hf + i];
+        pv[i] = sXD[ok + 6 + 3 * hf + i];
+        pn[i] = sXD[on + 3 * hf + i];
+        pw[i] = sXD[on + 6 + 3 * hf + i];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        auto pt = [&](const XD& p) {
+          const double v = p.x + al * p.d;
+          return base_pt ? p.x : v;
+        };
+        const double xq = pt(pq[i]), xv = pt(pv[i]), nq = pt(pn[i]), nv = pt(pw[i]);
+        const double dq = (xq + xv * P.dt) - nq;
+        const double dv = (xv + a[3 * hf + i] * P.dt) - nv;
+        eq += dq * dq;
+        ev += dv * dv;
+      }
     }
     o[3] = sqrt(eq) + sqrt(ev);
   }
