@@ -155,20 +155,29 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
   const double e0 = pe[0] - goal[0], e1 = pe[1] - goal[1], e2 = pe[2] - goal[2];
   o[0] = (last ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
   double vv = 0.0, uu = 0.0;
+  double v[6], u[6];
+  {
+    // the knot's v and u pairs: all 12 reads issued before their arithmetic
+    XD pv[6], pu[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const double vi = val(ok + 6 + i);
-    vv += vi * vi;
+    for (int i = 0; i < 6; ++i) {
+      pv[i] = sXD[ok + 6 + i];
+      pu[i] = sXD[last ? ok + 6 + i : ok + 12 + i];  // (the last knot has no u: unused)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double vi = pv[i].x + al * pv[i].d, ui = pu[i].x + al * pu[i].d;
+      v[i] = base_pt ? pv[i].x : vi;
+      u[i] = base_pt ? pu[i].x : ui;
+      vv += v[i] * v[i];
+    }
   }
   o[1] = P.dQ * vv;
   if (!last) {
-    double v[6], u[6], L[6][6], a[6];
+    double L[6][6], a[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      v[i] = val(ok + 6 + i);
-      u[i] = val(ok + 12 + i);
-      uu += u[i] * u[i];
-    }
+    for (int i = 0; i < 6; ++i) uu += u[i] * u[i];
     o[2] = P.R * uu;
     forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark);
     asm volatile("" ::: "memory");  // re-read the knot values from LDS below
@@ -332,9 +341,14 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
         double dd = 0.0;
+        XD p0[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) p0[i] = sXD[i];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-          const double t = val(i) - sXD[i].x;
+          const double vi = p0[i].x + al * p0[i].d;
+          const double t = (base_pt ? p0[i].x : vi) - p0[i].x;
           dd += t * t;
         }
         o[3] += sqrt(dd);
