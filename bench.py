@@ -353,6 +353,21 @@ def main():
                            "bytes_per_solve": ab["solve"]},
     }
     if cpu is not None:
+        # parity at bench scale: the C++ port on exactly the GPU's inputs (all B problems of
+        # this rank), against the last timed step's output and stats
+        from oracle import cpu as cpu_port
+
+        gpu_xu = t_out.cpu().numpy()
+        ref_xu, _, ref_alphas, _ = cpu_port.solve(xcur, goals, XU, N, nthreads=args.cpu_threads)
+        rel = np.linalg.norm(gpu_xu - ref_xu, axis=1) / np.maximum(np.linalg.norm(ref_xu, axis=1), 1e-300)
+        ga = st["alphas"][:, :ref_alphas.shape[1]]
+        used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
+        used_c = ~np.isnan(ref_alphas)
+        same_alpha = np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == ref_alphas, True), axis=1)
+        cpu["parity_vs_port"] = {
+            "problems": int(B), "alpha_sequence_agreement": float(same_alpha.mean()),
+            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
+            "gate": "SURVEY.md 8d: end-to-end XU rel. err <= 1e-4, alpha agreement reported separately"}
         fl = cpu.pop("flops")
         fl_dom = {"k_linearize": fl["linearize_per_iter"], "k_riccati": fl["riccati_per_iter"]}.get(dom)
         if fl_dom is not None:
