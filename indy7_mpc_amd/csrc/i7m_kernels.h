@@ -260,10 +260,15 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
   // (c0 already offset by this wave's share of the round; `store` false: compute only)
   auto reduce_store = [&](double o[4], int c0, bool store) {
     if (pow2) {
-      // tree-sum the N knots of each candidate slot with shuffles (segments of width N)
+      // tree-sum the N knots of each candidate slot with shuffles (segments of width N); the
+      // four terms' shuffles of one level are issued together (one LDS round trip per level)
+      for (int off = N >> 1; off >= 1; off >>= 1) {
+        double t[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        for (int off = N >> 1; off >= 1; off >>= 1) o[j] += __shfl_xor(o[j], off, 64);
+        for (int j = 0; j < 4; ++j) t[j] = __shfl_xor(o[j], off, 64);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += t[j];
+      }
       if (store && k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
     } else {
       part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
