@@ -76,6 +76,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+// two minima at once: both shuffles of a level in flight together
+__device__ __forceinline__ void wave_min2(double& a, double& b) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ta = __shfl_xor(a, off, 64), tb = __shfl_xor(b, off, 64);
+    a = fmin(a, ta);
+    b = fmin(b, tb);
+  }
+}
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
@@ -182,8 +191,7 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
       }
     }
   }
-  ap = wave_min(ap);
-  ad = wave_min(ad);
+  wave_min2(ap, ad);
   double acc = 0.0;
   for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
     double dv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U];

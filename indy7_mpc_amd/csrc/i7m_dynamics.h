@@ -172,17 +172,28 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
 #pragma unroll
     for (int k = 0; k < 6; ++k) f[5][k] = f[5][k] - cst<T>(fext6[k]);
   }
+  // a parked link's force is read back one link ahead (during the previous link's transform),
+  // so the LDS reads are in flight while that arithmetic runs
+  double pk[6];
+  if (NLDS == 6) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pk[k] = fs[(30 + k) * 64];
+  }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     __builtin_amdgcn_sched_barrier(0);
     if (i < NLDS) {
       if (i == 5) {  // the tip: no child contribution; the external wrench acts here
 #pragma unroll
-        for (int k = 0; k < 6; ++k) f[5][k] = cst<T>(fs[(30 + k) * 64]) - cst<T>(fext6 ? fext6[k] : 0.0);
+        for (int k = 0; k < 6; ++k) f[5][k] = cst<T>(pk[k]) - cst<T>(fext6 ? fext6[k] : 0.0);
       } else {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) f[i][k] = cst<T>(fs[(6 * i + k) * 64]) + f[i][k];
+        for (int k = 0; k < 6; ++k) f[i][k] = cst<T>(pk[k]) + f[i][k];
       }
+    }
+    if (i > 0 && i - 1 < NLDS) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pk[k] = fs[(6 * (i - 1) + k) * 64];
     }
     tau[i] = f[i][5];
     if (i > 0) {

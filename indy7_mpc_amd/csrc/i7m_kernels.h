@@ -246,9 +246,22 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
   double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
   __shared__ double merit[9];
   {
-    for (int e = threadIdx.x; e < P.T; e += 64 * W) {
-      const double xv = X[e];
-      sXD[e] = XD{xv, S[e] - xv};
+    // chunks of 6 entries per lane with every load issued before the first use (the plain loop
+    // waited out a global-memory round trip per entry: ~9 per wave at N = 32)
+    constexpr int SU = 6;
+    for (int e0 = threadIdx.x; e0 < P.T; e0 += 64 * W * SU) {
+      double xv[SU], sv[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int e = min(e0 + 64 * W * u, P.T - 1);
+        xv[u] = X[e];
+        sv[u] = S[e];
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int e = e0 + 64 * W * u;
+        if (e < P.T) sXD[e] = XD{xv[u], sv[u] - xv[u]};
+      }
     }
   }
   const double alphas[NALPHA] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
