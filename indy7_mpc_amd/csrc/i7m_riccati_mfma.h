@@ -168,6 +168,25 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     oK[s] = (u < 6 && lr < 13) ? MO_KT + 13 * u + lr : MO_ZERO;
   }
 
+  constexpr int SE = BOX ? 176 : 140;  // stash length
+  // stash element e of stage k lives at base(e) + k * stride(e): resolved once per lane for its
+  // three elements, so the per-stage loads are one multiply-add each (no divergent selects)
+  auto base_of = [&](int e, int& stride) -> const double* {
+    if (e < MO_QP) { stride = LIN_STRIDE; return LINb + e; }
+    if (e < MO_SIG) { stride = QPD_STRIDE; return QB + (e - MO_QP); }
+    stride = 18;
+    if (e < MO_HB) return bsig + (long)b * P.T + (e - MO_SIG);
+    return bh + (long)b * P.T + (e - MO_HB);
+  };
+  const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
+  int st0, st1, st2;
+  const double* sb0 = base_of(l, st0);
+  const double* sb1 = base_of(l + 64, st1);
+  const double* sb2 = base_of(e2, st2);
+  // (the first stage's stash is requested before the terminal record, so its latency overlaps
+  // the record's own loads)
+  double p0 = sb0[(long)(N - 2) * st0], p1 = sb1[(long)(N - 2) * st1], p2 = sb2[(long)(N - 2) * st2];
+
   // ---- terminal cost-to-go V~ = Q~_{N-1}: the terminal knot's record from cost and XU
   {
     const double* ct = CB + (N - 1) * COST_STRIDE;
@@ -191,23 +210,6 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   d4 V;
 #pragma unroll
   for (int i = 0; i < 4; ++i) V[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
-
-  constexpr int SE = BOX ? 176 : 140;  // stash length
-  // stash element e of stage k lives at base(e) + k * stride(e): resolved once per lane for its
-  // three elements, so the per-stage loads are one multiply-add each (no divergent selects)
-  auto base_of = [&](int e, int& stride) -> const double* {
-    if (e < MO_QP) { stride = LIN_STRIDE; return LINb + e; }
-    if (e < MO_SIG) { stride = QPD_STRIDE; return QB + (e - MO_QP); }
-    stride = 18;
-    if (e < MO_HB) return bsig + (long)b * P.T + (e - MO_SIG);
-    return bh + (long)b * P.T + (e - MO_HB);
-  };
-  const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
-  int st0, st1, st2;
-  const double* sb0 = base_of(l, st0);
-  const double* sb1 = base_of(l + 64, st1);
-  const double* sb2 = base_of(e2, st2);
-  double p0 = sb0[(long)(N - 2) * st0], p1 = sb1[(long)(N - 2) * st1], p2 = sb2[(long)(N - 2) * st2];
 
   for (int k = N - 2; k >= 0; --k) {
     lds_sync();
