@@ -394,6 +394,25 @@ __device__ __forceinline__ void aba_deriv_column(const DevModel& Md, const doubl
   chol6_solve(L, out);
 }
 
+// Joint-6 origin in the world frame only (no Jacobian), by Horner's rule from the tip:
+// p = t_0 + R_0 (t_1 + R_1 (... + R_4 t_5)), R_i = Rp_i Rz(q_i): ~16 ops per joint instead of the
+// rotation-chain composition's ~48 (same point as fk_jac to rounding).
+__device__ __forceinline__ void fk_pos(const DevModel& Md, const double c[6], const double s[6], double p[3]) {
+  double w[3] = {Md.tp[5][0], Md.tp[5][1], Md.tp[5][2]};
+#pragma unroll
+  for (int i = 4; i >= 0; --i) {
+    const double x[3] = {c[i] * w[0] - s[i] * w[1], s[i] * w[0] + c[i] * w[1], w[2]};
+    double y[3];
+    rp(Md.Rp[i], x, y);
+    w[0] = Md.tp[i][0] + y[0];
+    w[1] = Md.tp[i][1] + y[1];
+    w[2] = Md.tp[i][2] + y[2];
+  }
+  p[0] = w[0];
+  p[1] = w[1];
+  p[2] = w[2];
+}
+
 // World-frame forward kinematics of the joint-6 origin and its LOCAL_WORLD_ALIGNED linear
 // Jacobian (rows 0..2).  J may be null.
 __device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], const double s[6], double p[3],

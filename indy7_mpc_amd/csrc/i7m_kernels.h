@@ -151,7 +151,7 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
     for (int i = 0; i < 6; ++i) q[i] = val(ok + i);
     sincos6(q, c, sn);
   }
-  fk_jac(Md, c, sn, pe, nullptr);
+  fk_pos(Md, c, sn, pe);
   const double e0 = pe[0] - goal[0], e1 = pe[1] - goal[1], e2 = pe[2] - goal[2];
   o[0] = (last ? P.QN : 1.0) * (e0 * e0 + e1 * e1 + e2 * e2);
   double vv = 0.0, uu = 0.0;
