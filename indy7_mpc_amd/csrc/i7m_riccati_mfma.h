@@ -70,11 +70,17 @@ __device__ __forceinline__ double row_shl6_f64(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// 1/d to full fp64 precision: v_rcp_f64 + two Newton steps.
+// 1/d: v_rcp_f64 (about half the fp64 mantissa) + Newton steps, each doubling the correct
+// bits (I7M_RCP_NR, default 1: within ~2 ulp; 2 were used before, 1 is off the pivot chain of
+// every Gauss-Jordan step).
+#ifndef I7M_RCP_NR
+#define I7M_RCP_NR 1
+#endif
 __device__ __forceinline__ double rcp_nr(double d) {
   double y = __builtin_amdgcn_rcp(d);
-  y = y * (2.0 - d * y);
-  return y * (2.0 - d * y);
+#pragma unroll
+  for (int i = 0; i < I7M_RCP_NR; ++i) y = fma(y, fma(-d, y, 1.0), y);
+  return y;
 }
 
 // ABL (diagnostic builds only, results invalid; I7M_ABLATE in i7m_api.hip maps onto them):
