@@ -111,8 +111,8 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // SPEC: Indy7 constants baked in (kIndy7Model, generated from the URDF) instead of read from Mg.
 // k_linesearch register budget: 2 waves/SIMD (<= 256 VGPRs) with the forces of
 // links 0..2 parked in LDS and XU / sol staged in LDS: 18.3 KB LDS per wave at N = 32, i.e. 8
-// waves per CU.  Measured 151 -> 132 us (1 wave/SIMD before); staging matters more than the
-// ~90 B/lane of spill the 2-wave target leaves.
+// waves per CU.  Measured 151 -> 132 us (1 wave/SIMD before); now ~236 VGPRs, no VGPR spill
+// (the ~120 SGPRs the baked constants need spill to VGPR lanes: ~6 % of the round's VALU).
 constexpr int LS_NLDS = 3;  // links whose RNEA forces k_linesearch parks in LDS
 // per-wave LDS parking of k_linesearch (RNEA forces; the non-power-of-2 reduction reuses it)
 constexpr int LS_PARK = 6 * LS_NLDS * 64 > 256 ? 6 * LS_NLDS * 64 : 256;
@@ -127,9 +127,9 @@ struct alignas(16) XD {
 // Merit terms of one (candidate, knot) lane of k_linesearch: qcost, vcost, ucost and the
 // integrator error (src/osqp_sqp.py:13-47) at the line-search point XU + al (sol - XU)
 // (src/osqp_sqp.py:60), from the LDS copies of XU / sol; the knot values are re-read from LDS
-// where used instead of being held in registers across the dynamics.  (As a separate inlined
-// function the kernel allocates spill-free at 249 VGPRs; written in the round loop it spilled,
-// 115 -> 110 us.)
+// where used instead of being held in registers across the dynamics, each group of reads issued
+// ahead of its arithmetic.  (As a separate inlined function the kernel allocates spill-free;
+// written in the round loop it spilled, 115 -> 110 us.)
 template <bool SPEC>
 __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, const SolveParams& P, const int k,
                                                       const bool last, const bool base_pt, const double al,
