@@ -212,7 +212,21 @@ def main():
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo announces its peer connections on the C-level stdout; keep stdout for the one JSON
+        # line (the announcement goes to stderr instead)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+    # one rank per GPU (LOCAL_RANK); with fewer visible GPUs than ranks (a rehearsal of the
+    # multi-rank path on a small box) ranks share devices round-robin
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev > 0 else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
