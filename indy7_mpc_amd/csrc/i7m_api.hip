@@ -24,6 +24,12 @@
 
 using namespace i7m;
 
+// i7m_lin_tu.hip (its own translation unit: a different machine-scheduler setting)
+void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* model,
+                                 const void* params, const double* xu, const double* goals, const double* fext,
+                                 const int* active, double* lin, double* cost, double* qpd, int* init_active,
+                                 void* init_stats);
+
 static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
 
 namespace {
@@ -229,12 +235,8 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
   return timed(h, s, I7M_K_LIN, [&](hipEvent_t ea, hipEvent_t eb) {
-    if (h->spec)
-      hipExtLaunchKernelGGL(k_linearize<true>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost, W.qpd, init_active, init_stats);
-    else
-      hipExtLaunchKernelGGL(k_linearize<false>, dim3(grid), dim3(64), 0, s, ea, eb, 0, h->d_model, P, xu, goals, W.fext, active,
-                         W.lin, W.cost, W.qpd, init_active, init_stats);
+    i7m_launch_linearize_kernel(h->spec, grid, s, ea, eb, h->d_model, &P, xu, goals, W.fext, active, W.lin, W.cost, W.qpd,
+                                init_active, init_stats);
   });
 }
 

@@ -1,0 +1,36 @@
+// i7m_lin_tu.hip — k_linearize in a translation unit of its own, so that it can be compiled
+// with the max-ILP machine scheduler (-mllvm -amdgpu-sched-strategy=max-ilp; __graft_entry__
+// builds this file with it and the rest of the library with the default).  Measured at B = 4096,
+// N = 32: k_linearize 133.8 -> 130.1 us with max-ILP, while the same flag costs k_riccati_mfma
+// 1.6 us — hence the split.
+//
+// The kernel headers define non-template kernels and device functions too; included inside an
+// anonymous namespace here, this unit's copies stay internal and do not collide with
+// i7m_api.hip's at link time.  The launcher below is the only external symbol, with builtin
+// parameter types only.
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cmath>
+
+namespace {
+#include "i7m_linearize.h"
+}  // namespace
+
+// Launch of k_linearize (the model-specialised or the generic instantiation) with the dispatch
+// events of i7m_api.hip's kernel timing (ea / eb may be null).  model: DevModel*, params:
+// SolveParams*, init_stats: ProblemStats* (i7m_kernels.h).
+void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* model,
+                                 const void* params, const double* xu, const double* goals, const double* fext,
+                                 const int* active, double* lin, double* cost, double* qpd, int* init_active,
+                                 void* init_stats) {
+  const i7m::DevModel* M = static_cast<const i7m::DevModel*>(model);
+  const i7m::SolveParams& P = *static_cast<const i7m::SolveParams*>(params);
+  i7m::ProblemStats* st = static_cast<i7m::ProblemStats*>(init_stats);
+  if (spec)
+    hipExtLaunchKernelGGL(i7m::k_linearize<true>, dim3(grid), dim3(64), 0, s, ea, eb, 0, M, P, xu, goals, fext, active, lin,
+                          cost, qpd, init_active, st);
+  else
+    hipExtLaunchKernelGGL(i7m::k_linearize<false>, dim3(grid), dim3(64), 0, s, ea, eb, 0, M, P, xu, goals, fext, active, lin,
+                          cost, qpd, init_active, st);
+}
