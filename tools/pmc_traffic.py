@@ -12,7 +12,15 @@ import collections
 import csv
 import json
 import os
+import re
 import statistics
+
+
+def kernel_name(full):
+    """Short kernel name from the demangled symbol (also for kernels in an anonymous namespace,
+    e.g. `void (anonymous namespace)::i7m::k_linearize<true>(...)`)."""
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", full)
+    return m.group(1) if m else full.split("(")[0].split("<")[0].split("::")[-1]
 
 
 # kernel symbol -> the timing id bench.py reports (include/indy7_mpc.h I7M_K_*)
@@ -24,7 +32,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r.get("Counter_Name") != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
+        name = kernel_name(r["Kernel_Name"])
         name = CANON.get(name, name)
         grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
         vals[(name, grid)].append(float(r["Counter_Value"]))

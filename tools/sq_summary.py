@@ -13,6 +13,14 @@ import argparse
 import collections
 import csv
 import json
+import re
+
+
+def kernel_name(full):
+    """Short kernel name from the demangled symbol (also for kernels in an anonymous namespace,
+    e.g. `void (anonymous namespace)::i7m::k_linearize<true>(...)`)."""
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", full)
+    return m.group(1) if m else full.split("(")[0].split("<")[0].split("::")[-1]
 
 CANON = {"k_riccati_mfma": "k_riccati"}
 
@@ -25,7 +33,7 @@ def main():
     a = ap.parse_args()
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(a.csv)):
-        name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
+        name = kernel_name(r["Kernel_Name"])
         name = CANON.get(name, name)
         grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
         want = -(-a.batch * a.N // 10) * 64 if name == "k_linearize" else a.batch * 64

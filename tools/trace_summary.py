@@ -9,8 +9,16 @@ ceil(B*N/10)*64 for k_linearize): bench.py also runs B = 1 and host-to-host solv
 import collections
 import csv
 import json
+import re
 import statistics
 import sys
+
+
+def kernel_name(full):
+    """Short kernel name from the demangled symbol (also for kernels in an anonymous namespace,
+    e.g. `void (anonymous namespace)::i7m::k_linearize<true>(...)`)."""
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", full)
+    return m.group(1) if m else full.split("(")[0].split("<")[0].split("::")[-1]
 
 CANON = {"k_riccati_mfma": "k_riccati"}
 
@@ -18,7 +26,7 @@ CANON = {"k_riccati_mfma": "k_riccati"}
 def main(path, batch=None, N=32):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
+        name = kernel_name(r["Kernel_Name"])
         name = CANON.get(name, name)
         if batch is not None and name.startswith("k_"):
             grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
