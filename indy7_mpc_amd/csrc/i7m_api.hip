@@ -265,6 +265,7 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       case 11: launch_riccati_mfma<24>(s, ea, eb, W, P, xu, xs, active, sol); break;    // + lin slot 0
       case 13: launch_riccati_mfma<32>(s, ea, eb, W, P, xu, xs, active, sol); break;    // rollout dead
       case 18: launch_riccati_mfma<448>(s, ea, eb, W, P, xu, xs, active, sol); break;   // rollout chain only
+      case 19: launch_riccati_mfma<513>(s, ea, eb, W, P, xu, xs, active, sol); break;   // phase timestamps, no rollout
       default: launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
     }
   });

@@ -89,7 +89,8 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // (cache-resident), bit 4 the rollout's lin re-reads likewise, bit 5 drops the rollout's
 // stores (the compiler then drops the rollout's arithmetic), bit 6 feeds x instead of u to the
 // rollout's B u term (shorter chain), bit 7 skips the rollout's LDS staging, bit 8 keeps only
-// the last stage's stores; used to split the kernel's time.
+// the last stage's stores, bit 9 writes per-stage phase timestamps (s_memtime) of problem 0
+// into sol (tools/ric_phases.py); used to split the kernel's time.
 // BOX: the interior-point Newton step of the box-constrained QP (oracle/box_ipm.py): the same
 // QP with Hessian P + diag(Sigma) and linear term g + h, Sigma and h given per variable in
 // bsig / bh (B, T).  The equality rows are unchanged, so the result is the Newton iterate
@@ -217,8 +218,16 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
   for (int i = 0; i < 4; ++i) V[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
 
+  // ABL bit 9 (diagnostic): per-stage phase timestamps (s_memtime) of problem 0 into sol
+  long long tm0 = 0, tm1 = 0, tm2 = 0, tm3 = 0, ta = 0, tb = 0, td = 0, te = 0, tp = 0;
+  auto tstamp = [](double dep) -> long long {
+    asm volatile("" ::"v"(dep));
+    return (long long)__builtin_amdgcn_s_memtime();
+  };
   for (int k = N - 2; k >= 0; --k) {
     lds_sync();
+    if (ABL & 512) tm0 = tstamp(V[0]);
+    if (ABL & 512) tp = tstamp(p0 + p1 + p2);
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
     if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
@@ -239,11 +248,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     }
     // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
     // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
+    if (ABL & 512) ta = tstamp(bA[0] + bA[1] + bA[2] + bA[3] + bB[0] + bB[1] + Qi[0] + Ri[0] + Ni[0]);
     d4 W0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
 #pragma unroll
     for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
+    if (ABL & 512) tb = tstamp(W0[0] + W0[1] + W0[2] + W0[3]);
     d4 Z00 = Qi;
     if (lq == 0) Z00[3] += W0[3];
 #pragma unroll
@@ -254,8 +265,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     W1 = mfma(V[2], bB[1], W1);
     d4 Z11 = mfma(bB[0], W1[1], Ri);
     Z11 = mfma(bB[1], W1[2], Z11);
+    if (ABL & 512) tm1 = tstamp(bA[0] + bA[1] + bA[2] + bA[3] + Qi[0] + Ri[0] + Ni[0]);
     d4 Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
+    if (ABL & 512) tm2 = tstamp(Z10[0] + Z10[1] + Z11[0] + Z11[1]);
     double* kk = KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE;
     if ((ABL & 4) && !BOX) {
       // (Diagnostic alternative, I7M_ABLATE=8: measured 5 us slower per launch at B = 1 and
@@ -326,6 +339,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
       for (int i = 0; i < 6; ++i)
         E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : (cc < 19 ? sh[MO_G + 13 * i + (cc - 6)] : (i == cc - 19 ? 1.0 : 0.0));
+      if (ABL & 512) td = tstamp(E[0] + E[1] + E[2] + E[3] + E[4] + E[5]);
 #pragma unroll
       for (int p = 0; p < 6; ++p) {
         double Pc[6];
@@ -336,6 +350,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
         for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
       }
+      if (ABL & 512) te = tstamp(E[0] + E[1] + E[2] + E[3] + E[4] + E[5]);
       if (l >= 6 && l < 19) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (l - 6)] = -E[i];
@@ -346,8 +361,23 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         for (int i = 0; i < 6; ++i) hk[6 * i + (l - 19)] = E[i];
       }
       lds_sync();
+      if (ABL & 512) tm3 = tstamp(E[0]);
       V = mfma(sh[oK[0]], Z10[0], Z00);
       V = mfma(sh[oK[1]], Z10[1], V);
+      if (ABL & 512) {
+        const long long tm4 = tstamp(V[0] + V[1] + V[2] + V[3]);
+        if (b == 0 && l == 0) {
+          double* o = sol + 8 * k;
+          o[0] = (double)(ta - tp);    // stash LDS round trip + operand reads (+ MFMA chains)
+          o[2] = (double)(tp - tm0);   // the stash loads of the stage (issued a stage ahead)
+          o[1] = (double)(tb - ta);    // W0 chain
+          o[3] = (double)(tm2 - tm1);  // G~ issue
+          o[4] = (double)(td - tm2);   // H, G~ results -> LDS -> per-lane columns
+          o[5] = (double)(te - td);    // six pivots
+          o[6] = (double)(tm3 - te);   // K~ -> LDS
+          o[7] = (double)(tm4 - tm3);  // V~ update
+        }
+      }
       kk[l] = sh[MO_KT + l];
       if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
     }
