@@ -26,25 +26,66 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector = FP64 matrix, AMD spec (not in
 
 
 def algorithmic_bytes(N: int):
-    """Compulsory HBM bytes per problem per launch of each kernel (fp64): what the kernel must
-    read and write, nothing re-read; and per solve (8*(2*(18N-6)+12+3N) = 312 N)."""
+    """SURVEY.md §8d's algorithmic (compulsory) HBM bytes of one solve, fp64:
+    8 * (2 (18N - 6) + 12 + 3N) = 312 N  (XU in and out, xcur, goals).  This is the per-unit
+    figure of the roofline of record: every kernel's `achieved` is 312 N x the problems its
+    launch processes / its average launch time."""
+    return 8 * (2 * (18 * N - 6) + 12 + 3 * N)
+
+
+def intermediate_bytes(N: int):
+    """What each kernel of the 3-kernel pipeline reads and writes per problem per launch
+    INCLUDING its HBM-resident intermediates (lin, cost, QP records, gains, sol): the traffic the
+    pipeline's structure implies, as opposed to the compulsory 312 N; reported for context."""
     T = 18 * N - 6
     lin = (N - 1) * 114 * 8
     cost = N * 10 * 8
+    qpd = (N - 1) * 32 * 8
+    kbuf = (N - 1) * 84 * 8
     return {
-        "solve": 8 * (2 * T + 12 + 3 * N),
-        "k_linearize": 8 * (T + 3 * N) + lin + cost,          # XU, goals -> lin, cost
-        "k_riccati": 8 * (T + 12) + lin + cost + 8 * T,       # XU, xs, lin, cost -> sol
-        "k_linesearch": 8 * (2 * T + 3 * N) + 8 * T,          # XU, sol, goals -> XU
+        "k_linearize": 8 * (T + 3 * N) + lin + cost + qpd,                 # XU, goals -> lin, cost, qpd
+        "k_riccati": 8 * (T + 12) + 2 * lin + cost + qpd + 2 * kbuf + 8 * T,  # + gains out and back, lin twice
+        "k_linesearch": 8 * (2 * T + 3 * N) + lin + cost + 8 * T,          # XU, sol, goals, lin/cost base -> XU
     }
 
 
-def cpu_baseline(N: int, budget_s: float, seed: int, threads: int):
+def cpu_threads():
+    """Threads for the all-cores CPU leg: the CPUs this process may use — the GPU box allots a
+    share of the host (OMP_NUM_THREADS is set to it there, and worker pools must stay within it),
+    so the leg runs on that share, not on os.cpu_count()."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
+
+
+def build_native_port():
+    """Build the CPU port with -march=native for THIS host (oracle/cpp/Makefile `native`), so the
+    baseline uses the host's full vector ISA (AVX-512 on Zen 5); falls back to the portable
+    x86-64-v3 build if that fails.  Returns (library path, build description)."""
+    import subprocess
+
+    from oracle import cpu
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle", "cpp"), "-B", "native"], check=True, timeout=300,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        return cpu.LIB_NATIVE, "g++ -O3 -march=native -ffp-contract=off -fopenmp (built on this host)"
+    except Exception as e:  # noqa: BLE001 - reported, the portable build is the fallback
+        return cpu.LIB, f"g++ -O3 -march=x86-64-v3 (native build failed: {e})"
+
+
+def cpu_baseline(N: int, budget_s: float, seed: int, threads: int, native):
     """The C++ CPU port (oracle/cpp/i7m_cpu.cpp: the same SQP, exact KKT solve) timed on the
     host cores on a bounded sample of the same workload, single-threaded and with `threads`
-    OpenMP threads; plus the instrumented flop count of that algorithm on the sample."""
+    OpenMP threads; plus the instrumented flop count of that algorithm on the sample.
+    native: (library, build description) from build_native_port()."""
     from oracle import cpu
     from oracle.osqp_ref import synthetic_batch
+
+    lib_path, build_desc = native
+    cpu.load(lib_path)
 
     n = 64
     xcur, goals, XU = synthetic_batch(n, N, seed)
@@ -73,11 +114,16 @@ def cpu_baseline(N: int, budget_s: float, seed: int, threads: int):
     t5 = time.perf_counter()
     per_iter_lin = fl[0]["linearize"] / fl[0]["iters"]
     per_iter_qp = fl[0]["qp"] / fl[0]["iters"]
+    per_core = n / (t1 - t0)
     return {
-        "value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
+        "value": per_core, "unit": "solves/s", "cores": 1, "kind": "port",
         "sample": f"{n} solves (config-3 draws, N={N}, seed {seed}) by oracle/cpp/i7m_cpu.cpp, 1 thread, "
                   f"{t1 - t0:.1f}s",
-        "all_cores": {"value": nm / (t3 - t2), "cores": threads, "sample": f"{nm} solves, {threads} OpenMP threads"},
+        "build": build_desc,
+        "all_cores": {"value": nm / (t3 - t2), "cores": threads, "sample": f"{nm} solves, {threads} OpenMP threads",
+                      "host_cpu_count": os.cpu_count(),
+                      "note": "threads = the CPU share this process may use (affinity / OMP_NUM_THREADS; the GPU "
+                              "box allots a share of the host per GPU job), not os.cpu_count()"},
         "numpy_restatement": {"value": npy_n / (t5 - t4), "cores": 1,
                               "sample": f"{npy_n} solves by oracle/osqp_ref.py (numpy + scipy splu), {t5 - t4:.1f}s"},
         "cpu_model": _cpu_model(),
@@ -191,12 +237,12 @@ def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=cpu_threads())
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=30)
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (box QP) extra object")
@@ -207,6 +253,8 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # the CPU port for this host is compiled (a child process) before anything touches the GPU
+    native = build_native_port() if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
     import torch
     import torch.distributed as dist
 
@@ -311,10 +359,10 @@ def main():
     # host-to-host rate (numpy in -> H2D + kernels + D2H -> numpy out, i7m_solve): the PCIe-
     # inclusive figure of DESIGN.md §5, never `value`
     h2h = []
-    for i in range(4):
+    for i in range(23):  # 3 warm-up, >= 20 timed, median
         a = time.perf_counter()
         h.solve(xcur, goals, XU)
-        if i >= 1:
+        if i >= 3:
             h2h.append(time.perf_counter() - a)
 
     if rank != 0:
@@ -332,11 +380,12 @@ def main():
     # problems a launch actually processes: iteration 2 only runs the problems still active
     launches_per_step = max(dom_cnt // args.steps, 1)
     problems_per_launch = float(st["qp_iters"].sum()) / launches_per_step
-    achieved = problems_per_launch * ab[dom] / dom_avg_s / 1e9
+    achieved = problems_per_launch * ab / dom_avg_s / 1e9
     traffic = _pmc_traffic(dom, B, N)
+    alg_per_launch = problems_per_launch * ab
     per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c,
                       "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)} for k, (ms, c) in ktimes.items()}
-    cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads)
+    cpu = None if native is None else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads, native)
     c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1)
     c2 = None if (args.no_config2 or world > 1) else config2(model, stream, local, 200, 10)
     out = {
@@ -353,7 +402,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic (random start/goal states, SURVEY.md §8d, seed 45+1000*rank)",
         "config": {"workload": f"config3: B={B} problems/GPU, N={N}, full SQP (<=2 QP + line search), exact KKT",
-                   "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)"},
+                   "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)",
+                   "value_definition": "device-resident: inputs already in HBM, B*world*steps / (max over ranks of "
+                                       "the barrier-to-barrier wall time of K back-to-back solves); BASELINE.md 4's "
+                                       "host-to-host rate (H2D + solve + D2H, median) is host_to_host_solves_per_s"},
         "p50_latency_ms": statistics.median(step_ms),
         "kernel_timing": {"pass": "second pass of the same K steps with per-launch HIP events on each kernel's dispatch",
                           "value_during_event_pass": B * world * args.steps / elapsed_ev},
@@ -364,11 +416,14 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "algorithmic_bytes_per_problem": ab[dom], "problems_per_launch": problems_per_launch,
-                     "avg_launch_us": dom_avg_s * 1e6},
-        "roofline_solve": {"bound": "hbm", "achieved": value * ab["solve"] / 1e9, "peak": HBM_PEAK_GBS * world,
-                           "unit": "GB/s", "frac": value * ab["solve"] / 1e9 / (HBM_PEAK_GBS * world),
-                           "bytes_per_solve": ab["solve"]},
+                     "traffic_over_algorithmic": None if traffic is None else traffic / alg_per_launch,
+                     "algorithmic_bytes_per_problem": ab, "algorithmic_source": "SURVEY.md 8d: 312 N B per solve",
+                     "problems_per_launch": problems_per_launch, "avg_launch_us": dom_avg_s * 1e6,
+                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
+                     "intermediate_bytes_per_problem": intermediate_bytes(N).get(dom)},
+        "roofline_solve": {"bound": "hbm", "achieved": value * ab / 1e9, "peak": HBM_PEAK_GBS * world,
+                           "unit": "GB/s", "frac": value * ab / 1e9 / (HBM_PEAK_GBS * world),
+                           "bytes_per_solve": ab},
     }
     if cpu is not None:
         # parity at bench scale: the C++ port on exactly the GPU's inputs (all B problems of

@@ -118,13 +118,26 @@ int i7m_device_count(int* n);
 
 int i7m_create(const i7m_config* cfg, i7m_handle** out);
 void i7m_destroy(i7m_handle* h);
-int i7m_set_stream(i7m_handle* h, void* stream);  /* NULL -> the handle's own stream */
+/* NULL -> the handle's own stream, a blocking stream (ordered with the legacy null stream) */
+int i7m_set_stream(i7m_handle* h, void* stream);
 int i7m_synchronize(i7m_handle* h);
-/* Constant external wrench [force; torque] on joint 6, in its LOCAL frame (pinocchio f_ext
- * convention, src/gato_mpc_batch_sample.py:151-161), one per problem, used by every
- * dynamics evaluation of subsequent solves (linearisation and merit).  fext (B, 6);
- * NULL clears it.  Backs batch_sqp.set_external_wrench_batch (gato_controller.py:129). */
-int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext);
+
+/* External wrench [force; torque] acting on joint 6's body.  Frames:
+ *   I7M_WRENCH_WORLD  a spatial force in the WORLD frame, about the world origin, as the
+ *                     reference's callers draw it (gato_controller.py:77-81,120-129;
+ *                     src/gato_mpc_batch_sample.py:37-40).  Every dynamics evaluation converts
+ *                     it to joint 6's frame at that evaluation's configuration with
+ *                     oMi[6].actInv (src/gato_mpc_batch_sample.py:151-161,270-279), and the
+ *                     linearisation differentiates that conversion too.  i7m_rk4 converts once
+ *                     at the start configuration and holds it over the four stages, as the
+ *                     reference's host plant does (:270-279).
+ *   I7M_WRENCH_LOCAL  constant in joint 6's LOCAL frame (pinocchio's f_ext[6] as it is). */
+#define I7M_WRENCH_LOCAL 0
+#define I7M_WRENCH_WORLD 1
+/* One wrench per problem, used by every dynamics evaluation of subsequent solves
+ * (linearisation and merit).  fext (B, 6); NULL clears it.  Backs
+ * batch_sqp.set_external_wrench_batch (gato_controller.py:129). */
+int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext, int32_t frame);
 
 /* Full SQP solve, host buffers in/out (H2D + kernels + D2H, synchronous). */
 int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur, const double* goals,
@@ -164,11 +177,12 @@ int i7m_linesearch(i7m_handle* h, int32_t B, const double* xu, const double* xu_
 /* Kinematics / dynamics hooks, Bq independent queries (q,v,tau: (Bq,6)). */
 int i7m_eepos(i7m_handle* h, int32_t Bq, const double* q, double* p_out, double* J_out /*(Bq,3,6) or NULL*/);
 int i7m_aba(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau,
-            const double* fext /*(Bq,6) local spatial force on joint 6, or NULL*/, double* a_out);
+            const double* fext /*(Bq,6) spatial force on joint 6, or NULL*/, int32_t frame /*I7M_WRENCH_**/,
+            double* a_out);
 int i7m_aba_derivatives(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau,
                         double* dq /*(Bq,6,6)*/, double* dv, double* Minv, double* a);
 int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* u, double dt,
-            const double* fext, double* q_out, double* v_out);
+            const double* fext, int32_t frame, double* q_out, double* v_out);
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,

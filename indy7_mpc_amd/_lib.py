@@ -71,6 +71,8 @@ class i7m_config(C.Structure):
 
 
 QP_DIRECT, QP_BOX = 0, 1
+WRENCH_LOCAL, WRENCH_WORLD = 0, 1
+_FRAMES = {"local": WRENCH_LOCAL, "world": WRENCH_WORLD, WRENCH_LOCAL: WRENCH_LOCAL, WRENCH_WORLD: WRENCH_WORLD}
 BOX_Q, BOX_V, BOX_U = 1, 2, 4
 
 
@@ -104,7 +106,7 @@ SIGNATURES = [
     ("i7m_destroy", None, [_H]),
     ("i7m_set_stream", C.c_int, [_H, C.c_void_p]),
     ("i7m_synchronize", C.c_int, [_H]),
-    ("i7m_set_external_wrench", C.c_int, [_H, C.c_int32, _DP]),
+    ("i7m_set_external_wrench", C.c_int, [_H, C.c_int32, _DP, C.c_int32]),
     ("i7m_solve", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP, C.c_void_p]),
     ("i7m_solve_device", C.c_int, [_H, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                    C.c_void_p]),
@@ -114,9 +116,9 @@ SIGNATURES = [
     ("i7m_merit", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_linesearch", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_eepos", C.c_int, [_H, C.c_int32, _DP, _DP, _DP]),
-    ("i7m_aba", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, _DP]),
+    ("i7m_aba", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_aba_derivatives", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, _DP, _DP, _DP]),
-    ("i7m_rk4", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_double, _DP, _DP, _DP]),
+    ("i7m_rk4", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_double, _DP, C.c_int32, _DP, _DP]),
     ("i7m_set_timing", C.c_int, [_H, C.c_int]),
     ("i7m_get_kernel_times", C.c_int, [_H, _DP, C.POINTER(C.c_int32), C.c_int32]),
     ("i7m_reset_kernel_times", C.c_int, [_H]),
@@ -151,6 +153,12 @@ def _check(rc: int):
     if rc != 0:
         msg = _lib.i7m_last_error().decode(errors="replace")
         raise I7MError(f"libindy7mpc error {rc}: {msg}")
+
+
+def version() -> str:
+    """i7m_version(): build kind and the sha256 prefix of the sources it was compiled from
+    (__graft_entry__.src_hash)."""
+    return load().i7m_version().decode()
 
 
 def device_count() -> int:
@@ -288,12 +296,15 @@ class Handle:
         _check(self._lib.i7m_eepos(self._h, n, _ptr(q), _ptr(p), _ptr(J) if J is not None else None))
         return (p, J) if jacobian else p
 
-    def aba(self, q, v, tau, fext=None):
+    def aba(self, q, v, tau, fext=None, frame="local"):
+        """fext (n, 6) joint-6 wrench, in joint 6's frame ("local") or the world frame ("world",
+        converted at q by oMi[6].actInv)."""
         q, v, tau = (_f64(x).reshape(-1, NJ) for x in (q, v, tau))
         n = q.shape[0]
         a = np.empty((n, NJ))
         f = _f64(fext).reshape(n, 6) if fext is not None else None
-        _check(self._lib.i7m_aba(self._h, n, _ptr(q), _ptr(v), _ptr(tau), _ptr(f) if f is not None else None, _ptr(a)))
+        _check(self._lib.i7m_aba(self._h, n, _ptr(q), _ptr(v), _ptr(tau), _ptr(f) if f is not None else None,
+                                 _FRAMES[frame], _ptr(a)))
         return a
 
     def aba_derivatives(self, q, v, tau):
@@ -305,26 +316,29 @@ class Handle:
                                              _ptr(a)))
         return dq, dv, Mi, a
 
-    def rk4(self, q, v, u, dt, fext=None):
+    def rk4(self, q, v, u, dt, fext=None, frame="local"):
+        """utils.rk4 per row; a "world" wrench is converted once at the start q (the reference's
+        host plant, src/gato_mpc_batch_sample.py:270-279)."""
         q, v, u = (_f64(x).reshape(-1, NJ) for x in (q, v, u))
         n = q.shape[0]
         qo, vo = np.empty((n, NJ)), np.empty((n, NJ))
         f = _f64(fext).reshape(n, 6) if fext is not None else None
         _check(self._lib.i7m_rk4(self._h, n, _ptr(q), _ptr(v), _ptr(u), float(dt), _ptr(f) if f is not None else None,
-                                 _ptr(qo), _ptr(vo)))
+                                 _FRAMES[frame], _ptr(qo), _ptr(vo)))
         return qo, vo
 
     # ---- timing --------------------------------------------------------------------------
     def set_stream(self, stream_ptr: int):
         _check(self._lib.i7m_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
-    def set_external_wrench(self, fext):
-        """(B, 6) local joint-6 wrench per problem, or None to clear."""
+    def set_external_wrench(self, fext, frame="local"):
+        """(B, 6) joint-6 wrench per problem ([f; n]; frame "local" = joint 6's frame, "world" =
+        world frame about the origin, converted per configuration), or None to clear."""
         if fext is None:
-            _check(self._lib.i7m_set_external_wrench(self._h, 0, None))
+            _check(self._lib.i7m_set_external_wrench(self._h, 0, None, 0))
             return
         f = _f64(fext).reshape(-1, 6)
-        _check(self._lib.i7m_set_external_wrench(self._h, f.shape[0], _ptr(f)))
+        _check(self._lib.i7m_set_external_wrench(self._h, f.shape[0], _ptr(f), _FRAMES[frame]))
 
     def synchronize(self):
         _check(self._lib.i7m_synchronize(self._h))

@@ -7,9 +7,14 @@ Python surface — ``SQPSolverfloat_{1..256}`` with ``solve``, ``reset``, ``rese
 formulation of src/osqp_solver.py (fp64, exact QP) on the GPU.  N is taken from the XU width
 (traj_len = 18N - 6); goals use the GATO layout (B, 6N), first 3 of every 6 used.
 
-External wrench convention: [force; torque] on joint 6 in its LOCAL frame (pinocchio's f_ext,
-as src/gato_mpc_batch_sample.py:151-161 builds it); ``world_to_local_wrench`` converts a
-world-frame wrench at a given configuration the same way the reference's host code does.
+External wrench convention (``set_external_wrench_batch``): by default each row is what the
+reference's callers put there — a WORLD-frame force [f; n] (gato_controller.py:77-81,120-129 and
+src/gato_mpc_batch_sample.py:37-40 draw f and zero n), which the reference's own host code turns
+into joint 6's local frame at the current configuration with ``data.oMi[6].actInv``
+(src/gato_mpc_batch_sample.py:151-161,270-279).  Here every dynamics evaluation does that
+conversion at its own configuration (the linearisation differentiates it too), and
+``sim_forward`` converts once at the start state, like the reference's host rk4 plant.
+``frame="local"`` keeps a constant wrench in joint 6's frame instead (pinocchio's f_ext as is).
 """
 from __future__ import annotations
 
@@ -26,9 +31,12 @@ _SIZES = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 class _SQPSolverBatch:
     batch_size = 1
 
-    def __init__(self, model=None, device_id=0):
+    def __init__(self, model=None, device_id=0, wrench_frame="world"):
+        if wrench_frame not in ("world", "local"):
+            raise ValueError("wrench_frame must be 'world' or 'local'")
         self.model = model or default_model()
         self.device_id = device_id
+        self.wrench_frame = wrench_frame
         self._h = None
         self._key = None
         self._fext = np.zeros((self.batch_size, 6))
@@ -39,7 +47,7 @@ class _SQPSolverBatch:
             self._h = _lib.Handle(self.model, N=N, dt=dt, max_batch=self.batch_size, device_id=self.device_id)
             self._key = (N, dt)
             if np.any(self._fext):
-                self._h.set_external_wrench(self._fext)
+                self._h.set_external_wrench(self._fext, self.wrench_frame)
         return self._h
 
     def solve(self, XU_batch, dt, xcur_batch, eepos_goals_batch):
@@ -78,15 +86,16 @@ class _SQPSolverBatch:
         f = np.asarray(f_ext_batch, dtype=float).reshape(self.batch_size, 6)
         self._fext = f.copy()
         if self._h is not None:
-            self._h.set_external_wrench(self._fext)
+            self._h.set_external_wrench(self._fext, self.wrench_frame)
 
     def sim_forward(self, x, u, dt):
-        """One rk4 step of x (12,) under u (6,) for every wrench hypothesis -> (B, 12)."""
+        """One rk4 step of x (12,) under u (6,) for every wrench hypothesis -> (B, 12)
+        (gato_controller.py:109-118 compares these with the measured state)."""
         x = np.asarray(x, float).reshape(12)
         u = np.asarray(u, float).reshape(6)
         B = self.batch_size
         qo, vo = self._sim.rk4(np.tile(x[:6], (B, 1)), np.tile(x[6:], (B, 1)), np.tile(u, (B, 1)), float(dt),
-                               fext=self._fext)
+                               fext=self._fext, frame=self.wrench_frame)
         return np.hstack([qo, vo])
 
 

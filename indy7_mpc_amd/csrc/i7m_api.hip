@@ -18,17 +18,27 @@
 #include "../../include/indy7_mpc.h"
 #include "i7m_kernels.h"
 #include "i7m_linearize.h"
-#include "i7m_riccati.h"
 #include "i7m_riccati_mfma.h"
 #include "i7m_box.h"
+
+// Source hash of the tree this library was built from (__graft_entry__.build passes it), so
+// tests and smoke() can check that the loaded binary matches the sources they run against.
+#ifndef I7M_SRC_HASH
+#define I7M_SRC_HASH "unknown"
+#endif
+#ifdef I7M_DIAG
+#define I7M_BUILD_KIND "diag"
+#else
+#define I7M_BUILD_KIND "release"
+#endif
 
 using namespace i7m;
 
 // i7m_lin_tu.hip (its own translation unit: a different machine-scheduler setting)
 void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* model,
                                  const void* params, const double* xu, const double* goals, const double* fext,
-                                 const int* active, double* lin, double* cost, double* qpd, int* init_active,
-                                 void* init_stats);
+                                 bool fext_world, const int* active, double* lin, double* cost, double* qpd,
+                                 int* init_active, void* init_stats);
 
 static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
 
@@ -48,8 +58,6 @@ int fail(int code, const std::string& msg) {
       return fail(I7M_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                  \
   } while (0)
 
-constexpr int I7M_MAX_CHUNKS = 4;
-
 struct Timing {
   int kid;
   hipEvent_t a, b;
@@ -68,18 +76,17 @@ struct i7m_handle {
   double* d_qpd = nullptr;  // (max_batch, N-1, QPD_STRIDE) per-knot QP records (k_linearize -> k_riccati_mfma)
   int* d_active = nullptr;
   ProblemStats* d_stats = nullptr;
-  double* d_fext = nullptr;   // (max_batch, 6) local joint-6 wrench per problem
+  double* d_fext = nullptr;   // (max_batch, 6) joint-6 wrench per problem, frame fext_frame
+  int fext_frame = I7M_WRENCH_LOCAL;
   // I7M_QP_BOX (i7m_box.h): iterate, bound duals, Riccati inputs, predictor step; (max_batch, T)
   double *d_bx = nullptr, *d_bzl = nullptr, *d_bzu = nullptr, *d_bsig = nullptr, *d_bh = nullptr, *d_bdxa = nullptr;
   double *d_bhinv = nullptr, *d_bdh = nullptr;  // per-stage H^-1 (max_batch, N-1, 36); corrector dh (max_batch, T)
   IpmState* d_bst = nullptr;
   int* d_bact = nullptr;
-  uint32_t* d_ric_desc = nullptr;  // Riccati round descriptors (i7m_riccati.h)
-  int ric_impl = 0;                // 0: fp64 MFMA (i7m_riccati_mfma.h), 1: VALU rounds (i7m_riccati.h)
   // box QP: 1 k_ipm_fused<false> (default), 0 I7M_IPM=delta (k_ipm_fused<true>: the corrector
   // reuses the predictor's factorisation; measured slower), 2 I7M_IPM=split
   int ipm_mode = 1;
-  int ablate = 0;                  // diagnostic timing builds only (I7M_ABLATE), results invalid
+  int ablate = 0;                  // I7M_DIAG builds only (I7M_ABLATE): timing variants, results invalid
   bool spec = false;               // model == kIndy7Model: use the kernels with the constants baked in
   bool has_fext = false;
   size_t goal_cap = 0;
@@ -94,11 +101,7 @@ struct i7m_handle {
   unsigned long long graph_clock = 0;
   bool use_graph = false;  // I7M_GRAPH=1: capture the solve once per buffer set, replay it
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
-  // concurrent problem ranges (run_sqp): worker streams + fork/join events
-  int chunks = 0;  // 0: automatic (chunks_for), else I7M_CHUNKS
   int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
-  hipStream_t workers[I7M_MAX_CHUNKS] = {};
-  hipEvent_t fork = nullptr, join[I7M_MAX_CHUNKS] = {};
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -235,8 +238,8 @@ int launch_linearize(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePar
   if (knots == 0) return I7M_OK;
   const int grid = (int)((knots + KPW - 1) / KPW);
   return timed(h, s, I7M_K_LIN, [&](hipEvent_t ea, hipEvent_t eb) {
-    i7m_launch_linearize_kernel(h->spec, grid, s, ea, eb, h->d_model, &P, xu, goals, W.fext, active, W.lin, W.cost, W.qpd,
-                                init_active, init_stats);
+    i7m_launch_linearize_kernel(h->spec, grid, s, ea, eb, h->d_model, &P, xu, goals, W.fext,
+                                h->fext_frame == I7M_WRENCH_WORLD, active, W.lin, W.cost, W.qpd, init_active, init_stats);
   });
 }
 
@@ -251,12 +254,9 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
                    const double* xs, const int* active, double* sol) {
   if (P.B == 0) return I7M_OK;
   return timed(h, s, I7M_K_RICCATI, [&](hipEvent_t ea, hipEvent_t eb) {
-    if (h->ric_impl == 1) {
-      hipExtLaunchKernelGGL(k_riccati, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, h->d_ric_desc, xu, xs, W.lin, W.cost, active,
-                            W.kbuf, sol);
-      return;
-    }
-    // I7M_ABLATE -> ABL bits of riccati_mfma_body (diagnostic timing builds, results invalid)
+#ifdef I7M_DIAG
+    // I7M_ABLATE -> ABL bits of riccati_mfma_body (diagnostic timing builds, results invalid;
+    // compiled only into the -DI7M_DIAG library that tools/ load, never the shipping one)
     switch (h->ablate) {
       case 1: launch_riccati_mfma<1>(s, ea, eb, W, P, xu, xs, active, sol); break;      // no rollout
       case 2: launch_riccati_mfma<6>(s, ea, eb, W, P, xu, xs, active, sol); break;      // scaling for GJ
@@ -268,6 +268,9 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       case 19: launch_riccati_mfma<513>(s, ea, eb, W, P, xu, xs, active, sol); break;   // phase timestamps, no rollout
       default: launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
     }
+#else
+    launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
+#endif
   });
 }
 
@@ -283,22 +286,25 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
   const size_t lds = ls_lds_bytes(P.T, nw);
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
+  const bool fw = W.fext && h->fext_frame == I7M_WRENCH_WORLD;
   return timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
-    if (nw == 4 && h->spec)
-      hipExtLaunchKernelGGL((k_linesearch<true, 0, 4>), dim3(P.B), dim3(256), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol,
-                            goals, W.fext, active, st, alpha_out, iter, mode, ln, cs);
-    else if (nw == 4)
-      hipExtLaunchKernelGGL((k_linesearch<false, 0, 4>), dim3(P.B), dim3(256), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol,
-                            goals, W.fext, active, st, alpha_out, iter, mode, ln, cs);
-    else if (h->ablate == 4)
-      hipExtLaunchKernelGGL((k_linesearch<true, 1>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode, ln, cs);
-    else if (h->spec)
-      hipExtLaunchKernelGGL((k_linesearch<true, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode, ln, cs);
-    else
-      hipExtLaunchKernelGGL((k_linesearch<false, 0>), dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
-                         active, st, alpha_out, iter, mode, ln, cs);
+    auto go = [&](auto kern, int threads) {
+      hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(threads), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
+                            active, st, alpha_out, iter, mode, ln, cs);
+    };
+#ifdef I7M_DIAG
+    if (h->ablate == 4 && nw == 1) {
+      go(k_linesearch<true, 1>, 64);
+      return;
+    }
+#endif
+    if (nw == 4) {
+      if (h->spec) fw ? go(k_linesearch<true, 0, 4, true>, 256) : go(k_linesearch<true, 0, 4>, 256);
+      else fw ? go(k_linesearch<false, 0, 4, true>, 256) : go(k_linesearch<false, 0, 4>, 256);
+    } else {
+      if (h->spec) fw ? go(k_linesearch<true, 0, 1, true>, 64) : go(k_linesearch<true, 0, 1>, 64);
+      else fw ? go(k_linesearch<false, 0, 1, true>, 64) : go(k_linesearch<false, 0, 1>, 64);
+    }
   });
 }
 
@@ -363,63 +369,29 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   return I7M_OK;
 }
 
-// Number of concurrent problem ranges for a batch of B.  The three kernels are latency-bound
-// with different bottlenecks (MFMA chains, fp64 VALU chains, loads); ranges on separate streams
-// let waves of different kernels share a SIMD.
-int chunks_for(const i7m_handle* h, int B) {
-  int c = h->chunks;
-  if (c <= 0) c = 1;  // measured: 2-4 ranges give no gain at B = 4096
-  c = std::min(c, I7M_MAX_CHUNKS);
-  while (c > 1 && B / c < 256) --c;
-  return c;
-}
-
 // The SQP loop on device buffers: iteration 1 reads xu_in and its line search writes every
 // row of xu_out; later iterations update xu_out in place (xu_in == xu_out is allowed).  The
 // first linearisation also initialises the active flags and the stats (no memset launches).
+// (Splitting the batch into ranges on several streams, so that waves of different kernels share
+// a SIMD, was measured at 2-4 ranges and gave nothing: DESIGN.md §7.)
 int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const double* d_xs, const double* d_goals,
             int goal_stride, ProblemStats* d_st) {
-  const int C = chunks_for(h, B);
-  const long N = h->cfg.N, T = 18 * N - 6;
-  hipStream_t ss[I7M_MAX_CHUNKS];
-  int b0[I7M_MAX_CHUNKS + 1];
-  for (int c = 0; c <= C; ++c) b0[c] = (int)((long)B * c / C);
-  if (C == 1) {
-    ss[0] = h->stream;
-  } else {  // fork: every worker stream waits for the caller's stream
-    HIPCHK(hipEventRecord(h->fork, h->stream));
-    for (int c = 0; c < C; ++c) {
-      ss[c] = h->workers[c];
-      HIPCHK(hipStreamWaitEvent(ss[c], h->fork, 0));
-    }
-  }
+  const Bufs W = bufs_at(h, 0);
+  const SolveParams P = params_of(h, B, goal_stride);
+  hipStream_t s = h->stream;
   for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
-    for (int c = 0; c < C; ++c) {
-      const long o = b0[c];
-      const Bufs W = bufs_at(h, o);
-      SolveParams P = params_of(h, b0[c + 1] - b0[c], goal_stride);
-      double* xu = d_xu + o * T;
-      const double* xin = (it == 0 ? d_xu_in : d_xu) + o * T;
-      const double* xs = d_xs + o * 12;
-      const double* g = d_goals + o * N * goal_stride;
-      int* act = h->d_active + o;
-      int rc;
-      if (it == 0)
-        rc = launch_linearize(h, ss[c], W, P, xin, g, nullptr, act, d_st + o);
-      else
-        rc = launch_linearize(h, ss[c], W, P, xin, g, act);
-      if (rc) return rc;
-      const double* qsol = nullptr;
-      if ((rc = solve_qp(h, ss[c], W, P, xin, xs, act, h->d_sol + o * T, &qsol))) return rc;
-      if ((rc = launch_linesearch(h, ss[c], W, P, xin, xu, qsol, g, act, d_st + o, nullptr, it, 0, h->ablate != 6)))
-        return rc;
-    }
-  }
-  if (C > 1) {  // join
-    for (int c = 0; c < C; ++c) {
-      HIPCHK(hipEventRecord(h->join[c], ss[c]));
-      HIPCHK(hipStreamWaitEvent(h->stream, h->join[c], 0));
-    }
+    const double* xin = it == 0 ? d_xu_in : d_xu;
+    int rc;
+    if (it == 0)
+      rc = launch_linearize(h, s, W, P, xin, d_goals, nullptr, h->d_active, d_st);
+    else
+      rc = launch_linearize(h, s, W, P, xin, d_goals, h->d_active);
+    if (rc) return rc;
+    const double* qsol = nullptr;
+    if ((rc = solve_qp(h, s, W, P, xin, d_xs, h->d_active, h->d_sol, &qsol))) return rc;
+    if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, h->d_active, d_st, nullptr, it, 0,
+                                h->ablate != 6)))
+      return rc;
   }
   return I7M_OK;
 }
@@ -435,7 +407,7 @@ void drop_graphs(i7m_handle* h) {
 // sequence once.  Timing runs (events) and multi-range runs go direct.
 int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const double* d_xs, const double* d_goals,
                     int goal_stride, ProblemStats* d_st) {
-  if (!h->use_graph || h->timing || chunks_for(h, B) > 1)
+  if (!h->use_graph || h->timing)
     return run_sqp(h, B, d_xu_in, d_xu, d_xs, d_goals, goal_stride, d_st);
   const int hf = h->has_fext ? 1 : 0;
   i7m_handle::GraphEntry* hit = nullptr;
@@ -487,7 +459,7 @@ extern "C" {
 
 const char* i7m_last_error(void) { return g_err.c_str(); }
 
-const char* i7m_version(void) { return "indy7_mpc_amd 0.1 (gfx950, fp64)"; }
+const char* i7m_version(void) { return "indy7_mpc_amd 0.2 (gfx950, fp64, " I7M_BUILD_KIND ") src " I7M_SRC_HASH; }
 
 int i7m_device_count(int* n) {
   if (!n) return fail(I7M_EINVAL, "null");
@@ -555,23 +527,23 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     return rc;
   };
   if (hipSetDevice(h->dev) != hipSuccess) return bail(fail(I7M_EHIP, "hipSetDevice failed"));
-  if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess)
+  // the handle's own stream is a blocking one: it orders with the legacy null stream, so a caller
+  // that fills the inputs on the default (null) stream and never calls i7m_set_stream still has
+  // its copies ordered before the solve and the solve before its reads
+  if (hipStreamCreateWithFlags(&h->own, hipStreamDefault) != hipSuccess)
     return bail(fail(I7M_EHIP, "hipStreamCreate failed"));
   h->stream = h->own;
-  // developer knob for A/B profiling of the two QP kernels (default: MFMA)
-  if (const char* e = std::getenv("I7M_RICCATI")) h->ric_impl = (std::strcmp(e, "valu") == 0) ? 1 : 0;
+#ifdef I7M_DIAG
   if (const char* e = std::getenv("I7M_ABLATE")) h->ablate = std::atoi(e);
+#else
+  if (std::getenv("I7M_ABLATE"))
+    return bail(fail(I7M_EINVAL, "I7M_ABLATE is set, but this is the release library: the ablation "
+                                 "timing kernels exist only in the -DI7M_DIAG build (tools/)"));
+#endif
   if (const char* e = std::getenv("I7M_IPM"))
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
-  if (const char* e = std::getenv("I7M_CHUNKS")) h->chunks = std::atoi(e);
   if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
-  for (int c = 0; c < I7M_MAX_CHUNKS; ++c)
-    if (hipStreamCreateWithFlags(&h->workers[c], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->join[c], hipEventDisableTiming) != hipSuccess)
-      return bail(fail(I7M_EHIP, "worker stream creation failed"));
-  if (hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess)
-    return bail(fail(I7M_EHIP, "event creation failed"));
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
   // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
   const size_t scratch = std::max(Bm * T, (size_t)256 * 114);
@@ -584,7 +556,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_qpd, Bm * (N - 1) * QPD_STRIDE * 8) &&
             alloc((void**)&h->d_out, scratch * 8) &&
             alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
-            alloc((void**)&h->d_fext, Bm * 6 * 8) && alloc((void**)&h->d_ric_desc, RIC_DESC_WORDS * 4);
+            alloc((void**)&h->d_fext, Bm * 6 * 8);
   if (ok && cfg->qp_mode == I7M_QP_BOX)
     ok = alloc((void**)&h->d_bx, Bm * T * 8) && alloc((void**)&h->d_bzl, Bm * T * 8) &&
          alloc((void**)&h->d_bzu, Bm * T * 8) && alloc((void**)&h->d_bsig, Bm * T * 8) &&
@@ -592,10 +564,6 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
          alloc((void**)&h->d_bhinv, Bm * (N - 1) * 36 * 8) && alloc((void**)&h->d_bdh, Bm * T * 8) &&
          alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
-  std::vector<uint32_t> desc(RIC_DESC_WORDS);
-  build_riccati_desc(desc.data());
-  if (hipMemcpy(h->d_ric_desc, desc.data(), desc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-    return bail(fail(I7M_EHIP, "descriptor upload failed"));
   DevModel dm = make_dev_model(cfg->model);
   // the Indy7-specialised kernels are used only for a model bit-identical to the baked one
   h->spec = std::memcmp(&dm, &kIndy7Model, sizeof(DevModel)) == 0;
@@ -611,7 +579,7 @@ void i7m_destroy(i7m_handle* h) {
   (void)hipSetDevice(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_ric_desc, h->d_qpd,
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_qpd,
                   h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact,
                   h->d_bhinv, h->d_bdh};
   for (void* p : bufs)
@@ -622,14 +590,6 @@ void i7m_destroy(i7m_handle* h) {
   }
   for (auto e : h->pool) (void)hipEventDestroy(e);
   drop_graphs(h);
-  for (int c = 0; c < I7M_MAX_CHUNKS; ++c) {
-    if (h->workers[c]) {
-      (void)hipStreamSynchronize(h->workers[c]);
-      (void)hipStreamDestroy(h->workers[c]);
-    }
-    if (h->join[c]) (void)hipEventDestroy(h->join[c]);
-  }
-  if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
@@ -640,18 +600,23 @@ int i7m_set_stream(i7m_handle* h, void* stream) {
   return I7M_OK;
 }
 
-int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext) {
+int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext, int32_t frame) {
   if (!h) return fail(I7M_EINVAL, "null handle");
   if (!fext) {
     h->has_fext = false;
     return I7M_OK;
   }
+  if (frame != I7M_WRENCH_LOCAL && frame != I7M_WRENCH_WORLD)
+    return fail(I7M_EINVAL, "frame must be I7M_WRENCH_LOCAL or I7M_WRENCH_WORLD");
   if (B < 1 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "external wrench batch outside [1, max_batch]");
   HIPCHK(hipSetDevice(h->dev));
   HIPCHK(hipMemsetAsync(h->d_fext, 0, (size_t)h->cfg.max_batch * 6 * 8, h->stream));
   HIPCHK(hipMemcpyAsync(h->d_fext, fext, (size_t)B * 6 * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->has_fext = true;
+  h->fext_frame = frame;
+  // captured graphs hold the old wrench pointer / kernel choice
+  drop_graphs(h);
   return I7M_OK;
 }
 
@@ -758,7 +723,7 @@ int i7m_merit(i7m_handle* h, int32_t B, const double* xu, const double* xu_ref, 
   if ((rc = copy_in(h, h->d_aux, xu_ref, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
   hipLaunchKernelGGL(k_merit, dim3(B), dim3(64), 0, h->stream, h->d_model, P, h->d_xu, h->d_aux, h->d_goal,
-                     h->has_fext ? h->d_fext : nullptr, h->d_out);
+                     h->has_fext ? h->d_fext : nullptr, (int)(h->fext_frame == I7M_WRENCH_WORLD), h->d_out);
   HIPCHK(hipGetLastError());
   if ((rc = copy_out(h, out, h->d_out, (size_t)B * 5))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -810,7 +775,7 @@ int i7m_eepos(i7m_handle* h, int32_t Bq, const double* q, double* p_out, double*
 }
 
 int i7m_aba(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* tau, const double* fext,
-            double* a_out) {
+            int32_t frame, double* a_out) {
   if (!h) return fail(I7M_EINVAL, "null handle");
   if (Bq < 0 || !q || !v || !tau || !a_out) return fail(I7M_EINVAL, "bad arguments");
   HIPCHK(hipSetDevice(h->dev));
@@ -827,7 +792,7 @@ int i7m_aba(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
     if ((rc = copy_in(h, dtau, tau + 6 * o, 6 * (size_t)n))) return rc;
     if (fext && (rc = copy_in(h, df, fext + 6 * o, 6 * (size_t)n))) return rc;
     hipLaunchKernelGGL(k_aba, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_model, n, dq, dv, dtau,
-                       fext ? df : nullptr, h->d_sol);
+                       fext ? df : nullptr, (int)(frame == I7M_WRENCH_WORLD), h->d_sol);
     HIPCHK(hipGetLastError());
     if ((rc = copy_out(h, a_out + 6 * o, h->d_sol, 6 * (size_t)n))) return rc;
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -870,7 +835,7 @@ int i7m_aba_derivatives(i7m_handle* h, int32_t Bq, const double* q, const double
 }
 
 int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* u, double dt,
-            const double* fext, double* q_out, double* v_out) {
+            const double* fext, int32_t frame, double* q_out, double* v_out) {
   if (!h) return fail(I7M_EINVAL, "null handle");
   if (Bq < 0 || !q || !v || !u || !q_out || !v_out) return fail(I7M_EINVAL, "bad arguments");
   HIPCHK(hipSetDevice(h->dev));
@@ -889,7 +854,7 @@ int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
     if ((rc = copy_in(h, iu, u + 6 * o, 6 * (size_t)n))) return rc;
     if (fext && (rc = copy_in(h, iff, fext + 6 * o, 6 * (size_t)n))) return rc;
     hipLaunchKernelGGL(k_rk4, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_model, n, iq, iv, iu, dt,
-                       fext ? iff : nullptr, oq, ov);
+                       fext ? iff : nullptr, (int)(frame == I7M_WRENCH_WORLD), oq, ov);
     HIPCHK(hipGetLastError());
     if ((rc = copy_out(h, q_out + 6 * o, oq, 6 * (size_t)n))) return rc;
     if ((rc = copy_out(h, v_out + 6 * o, ov, 6 * (size_t)n))) return rc;

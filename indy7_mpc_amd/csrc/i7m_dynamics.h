@@ -413,6 +413,45 @@ __device__ __forceinline__ void fk_pos(const DevModel& Md, const double c[6], co
   p[2] = w[2];
 }
 
+// External wrench given in the WORLD frame (a spatial force [f; n] about the world origin, as
+// the reference's callers build it: pin.Force(f_ext[:3], f_ext[3:]), src/gato_mpc_batch_sample.py:
+// 155-158) -> the joint-6 LOCAL frame the dynamics take (pinocchio f_ext[6]):
+// data.oMi[6].actInv(world_force) (:160), i.e. f_l = R' f, n_l = R' (n - p x f), with (R, p) the
+// world placement of joint 6 at the configuration (c, s) = cos / sin(q).
+__device__ __forceinline__ void wrench_world_to_local(const DevModel& Md, const double c[6], const double s[6],
+                                                      const double* fw, double fl[6]) {
+  double R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  double p[3] = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double* Rp = Md.Rp[i];
+    const double* t = Md.tp[i];
+    double np_[3], RR[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[r][0] * t[0] + R[r][1] * t[1] + R[r][2] * t[2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) RR[r][q] = R[r][0] * Rp[q] + R[r][1] * Rp[3 + q] + R[r][2] * Rp[6 + q];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      R[r][0] = RR[r][0] * c[i] + RR[r][1] * s[i];
+      R[r][1] = RR[r][1] * c[i] - RR[r][0] * s[i];
+      R[r][2] = RR[r][2];
+      p[r] = np_[r];
+    }
+  }
+  const double f0 = fw[0], f1 = fw[1], f2 = fw[2];
+  const double m0 = fw[3] - (p[1] * f2 - p[2] * f1);
+  const double m1 = fw[4] - (p[2] * f0 - p[0] * f2);
+  const double m2 = fw[5] - (p[0] * f1 - p[1] * f0);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    fl[q] = R[0][q] * f0 + R[1][q] * f1 + R[2][q] * f2;
+    fl[3 + q] = R[0][q] * m0 + R[1][q] * m1 + R[2][q] * m2;
+  }
+}
+
 // World-frame forward kinematics of the joint-6 origin and its LOCAL_WORLD_ALIGNED linear
 // Jacobian (rows 0..2).  J may be null.
 __device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], const double s[6], double p[3],

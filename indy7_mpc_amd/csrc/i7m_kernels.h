@@ -4,7 +4,7 @@
 //
 //   k_linearize   (i7m_linearize.h) six lanes per knot: analytic world-frame derivatives of
 //                 the dynamics + cost linearisation.  Replaces src/osqp_solver.py:70-135.
-//   k_riccati     (i7m_riccati.h) one wavefront per problem: exact solve of the
+//   k_riccati_mfma (i7m_riccati_mfma.h) one wavefront per problem: exact solve of the
 //                 equality-constrained QP (src/osqp_solver.py:137-143), Riccati recursion.
 //   k_linesearch  one wavefront per problem, lanes = (candidate alpha, knot): merit of the
 //                 base point and of the backtracking alphas, several candidates per round,
@@ -70,7 +70,8 @@ __device__ __forceinline__ void cost_knot(const DevModel& Md, const SolveParams&
 // Merit pieces of one knot (src/osqp_sqp.py:13-47): qcost, vcost, ucost, integrator error.
 // x: 18 values of knot k (12 at the last knot), xn: the 12 state values of knot k+1.
 __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams& P, int k, const double* x,
-                                           const double* xn, const double* goal, const double* f6, double out[4]) {
+                                           const double* xn, const double* goal, const double* f6, bool fw,
+                                           double out[4]) {
   double c[6], s[6], p[3];
   sincos6(x, c, s);
   fk_jac(Md, c, s, p, nullptr);
@@ -88,7 +89,11 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 #pragma unroll
     for (int i = 0; i < 6; ++i) uu += x[12 + i] * x[12 + i];
     out[2] = P.R * uu;
-    double L[6][6], a[6];
+    double L[6][6], a[6], fl[6];
+    if (fw && f6) {
+      wrench_world_to_local(Md, c, s, f6, fl);
+      f6 = fl;
+    }
     forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
     double eq = 0.0, ev = 0.0;
 #pragma unroll
@@ -130,7 +135,8 @@ struct alignas(16) XD {
 // where used instead of being held in registers across the dynamics, each group of reads issued
 // ahead of its arithmetic.  (As a separate inlined function the kernel allocates spill-free;
 // written in the round loop it spilled, 115 -> 110 us.)
-template <bool SPEC>
+// FW: f6 is a world-frame wrench, converted to joint 6's frame at this knot's configuration.
+template <bool SPEC, bool FW = false>
 __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, const SolveParams& P, const int k,
                                                       const bool last, const bool base_pt, const double al,
                                                       const XD* sXD, const double* goal,
@@ -179,7 +185,13 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) uu += u[i] * u[i];
     o[2] = P.R * uu;
-    forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark);
+    if (FW && f6) {
+      double fl[6];
+      wrench_world_to_local(Md, c, sn, f6, fl);
+      forward_dynamics<LS_NLDS>(Md, c, sn, v, u, fl, L, a, fpark);
+    } else {
+      forward_dynamics<LS_NLDS>(Md, c, sn, v, u, f6, L, a, fpark);
+    }
     asm volatile("" ::: "memory");  // re-read the knot values from LDS below
     // the knot values in two halves of 12 LDS pair reads, each half issued before its
     // arithmetic (interleaved with it, the scheduler reused one register set and waited on each
@@ -216,7 +228,8 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
 // W waves per problem (small batches, where the GPU is otherwise idle): wave w evaluates the
 // candidate slots c0 + w R .. c0 + w R + R - 1 of each round, so W R candidates per round (all
 // eight alphas in one round at N = 32, W = 4).  Same first-accept rule, same merits.
-template <bool SPEC, int ABL = 0, int W = 1>
+// FW: fext is a world-frame wrench (I7M_WRENCH_WORLD), see ls_merit_terms.
+template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    const double* xu, double* xu_out, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
@@ -245,6 +258,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
   double* fpark = ls_dyn + 2 * P.T + w * LS_PARK;
   double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
   __shared__ double merit[9];
+  int step_nz = 0;  // does this lane stage a nonzero step entry sol - XU?
   {
     // chunks of 6 entries per lane with every load issued before the first use (the plain loop
     // waited out a global-memory round trip per entry: ~9 per wave at N = 32)
@@ -260,7 +274,11 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
         const int e = e0 + 64 * W * u;
-        if (e < P.T) sXD[e] = XD{xv[u], sv[u] - xv[u]};
+        if (e < P.T) {
+          const double d = sv[u] - xv[u];
+          sXD[e] = XD{xv[u], d};
+          step_nz |= (d != 0.0);
+        }
       }
     }
   }
@@ -268,7 +286,11 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
   const bool pow2 = (N & (N - 1)) == 0;
   const double* goal = goals + (long)b * N * P.goal_stride + (long)(k < N ? k : 0) * P.goal_stride;
   const double* f6 = fext ? fext + 6L * b : nullptr;
-  lds_sync();
+  // A step of exactly zero (sol == XU): every candidate point IS XU, so the reference's
+  // merit_new equals basemerit bit for bit and alpha = 1 is accepted (src/osqp_sqp.py:58-72).
+  // Decided here, not by comparing merits, because the base merit below comes from the
+  // linearisation and rounds differently from the candidate evaluation.
+  const bool zero_step = __syncthreads_or(step_nz) == 0;
   // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
   // (c0 already offset by this wave's share of the round; `store` false: compute only)
   auto reduce_store = [&](double o[4], int c0, bool store) {
@@ -300,7 +322,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
     lds_sync();
   };
   int cstart = 0;
-  if (lin) {
+  if (lin && !zero_step) {
     // base merit (src/osqp_sqp.py:52-55) from the linearisation of this XU: |e| (cost[9]) and
     // a = ABA(q, v, u) (lin[108..113]) per knot; slot 0 of the candidate layout
     const double* LB = lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -332,7 +354,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
     cstart = 1;
   }
   double base = 0.0;
-  int found = -1;
+  int found = zero_step ? 1 : -1;
   for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R * W) {
     const int cw = c0 + w * R;  // this wave's first candidate of the round
     const int cand = cw + slot;
@@ -354,7 +376,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
         o[3] = val(on + 6) + val(ok + 11);
       } else {
-        ls_merit_terms<SPEC>(Mg, P, k, last, base_pt, al, sXD, goal, f6, fpark + l, o);
+        ls_merit_terms<SPEC, FW>(Mg, P, k, last, base_pt, al, sXD, goal, f6, fpark + l, o);
       }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
@@ -422,7 +444,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
 __global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, SolveParams P,
                                               const double* __restrict__ xu, const double* __restrict__ xu_ref,
                                               const double* __restrict__ goals, const double* __restrict__ fext,
-                                              double* __restrict__ out) {
+                                              int fext_world, double* __restrict__ out) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
   const int l = threadIdx.x;
@@ -431,7 +453,7 @@ __global__ void __launch_bounds__(64) k_merit(const DevModel* __restrict__ Mg, S
   for (int k = l; k < P.N; k += 64) {
     double o[4];
     merit_knot(*Mg, P, k, X + 18 * k, (k < P.N - 1) ? X + 18 * (k + 1) : X, goals + (long)b * P.N * P.goal_stride + (long)k * P.goal_stride,
-               fext ? fext + 6L * b : nullptr, o);
+               fext ? fext + 6L * b : nullptr, fext_world != 0, o);
     part[k][0] = o[0]; part[k][1] = o[1]; part[k][2] = o[2]; part[k][3] = o[3];
   }
   lds_sync();
@@ -464,14 +486,20 @@ __global__ void __launch_bounds__(256) k_eepos(const DevModel* __restrict__ Mg, 
       for (int j = 0; j < 6; ++j) J[18L * i + 6 * r + j] = JJ[r][j];
 }
 
+// fext (n, 6) or null; fext_world: it is a world-frame wrench (converted at q), else local.
 __global__ void __launch_bounds__(256) k_aba(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
                                              const double* __restrict__ v, const double* __restrict__ tau,
-                                             const double* __restrict__ fext, double* __restrict__ a) {
+                                             const double* __restrict__ fext, int fext_world, double* __restrict__ a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double c[6], s[6], L[6][6], aa[6];
+  double c[6], s[6], L[6][6], aa[6], fl[6];
   sincos6(q + 6L * i, c, s);
-  forward_dynamics(*Mg, c, s, v + 6L * i, tau + 6L * i, fext ? fext + 6L * i : nullptr, L, aa);
+  const double* f6 = fext ? fext + 6L * i : nullptr;
+  if (f6 && fext_world) {
+    wrench_world_to_local(*Mg, c, s, f6, fl);
+    f6 = fl;
+  }
+  forward_dynamics(*Mg, c, s, v + 6L * i, tau + 6L * i, f6, L, aa);
   for (int r = 0; r < 6; ++r) a[6L * i + r] = aa[r];
 }
 
@@ -504,17 +532,24 @@ __global__ void __launch_bounds__(256) k_abad(const DevModel* __restrict__ Mg, i
 }
 
 // utils.rk4 (src/utils.py:3-18): 4 ABA evaluations, pin.integrate = q + v*dt.
+// fext_world: fext is a world-frame wrench, converted to joint 6's frame ONCE at the start
+// configuration q and held for the four stages, as the reference's host plant does
+// (src/gato_mpc_batch_sample.py:270-279: actInv at x_last, then rk4 with that local force).
 __global__ void __launch_bounds__(256) k_rk4(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
                                              const double* __restrict__ v, const double* __restrict__ u, double dt,
-                                             const double* __restrict__ fext, double* __restrict__ qo,
+                                             const double* __restrict__ fext, int fext_world, double* __restrict__ qo,
                                              double* __restrict__ vo) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double* f6 = fext ? fext + 6L * i : nullptr;
-  double q0[6], v0[6], uu[6], c[6], s[6], L[6][6];
+  double q0[6], v0[6], uu[6], c[6], s[6], L[6][6], fl[6];
   for (int r = 0; r < 6; ++r) { q0[r] = q[6L * i + r]; v0[r] = v[6L * i + r]; uu[r] = u[6L * i + r]; }
   double k1v[6], k2v[6], k3v[6], k4v[6], k2q[6], k3q[6], k4q[6], qq[6];
   sincos6(q0, c, s);
+  if (f6 && fext_world) {
+    wrench_world_to_local(*Mg, c, s, f6, fl);
+    f6 = fl;
+  }
   forward_dynamics(*Mg, c, s, v0, uu, f6, L, k1v);
   for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + v0[r] * dt / 2; k2q[r] = v0[r] + k1v[r] * dt / 2; }
   sincos6(qq, c, s);

@@ -20,17 +20,21 @@ namespace {
 // Launch of k_linearize (the model-specialised or the generic instantiation) with the dispatch
 // events of i7m_api.hip's kernel timing (ea / eb may be null).  model: DevModel*, params:
 // SolveParams*, init_stats: ProblemStats* (i7m_kernels.h).
+// fext_world: fext (non-null) is a world-frame wrench (k_linearize<., true>).
 void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* model,
                                  const void* params, const double* xu, const double* goals, const double* fext,
-                                 const int* active, double* lin, double* cost, double* qpd, int* init_active,
-                                 void* init_stats) {
+                                 bool fext_world, const int* active, double* lin, double* cost, double* qpd,
+                                 int* init_active, void* init_stats) {
   const i7m::DevModel* M = static_cast<const i7m::DevModel*>(model);
   const i7m::SolveParams& P = *static_cast<const i7m::SolveParams*>(params);
   i7m::ProblemStats* st = static_cast<i7m::ProblemStats*>(init_stats);
-  if (spec)
-    hipExtLaunchKernelGGL(i7m::k_linearize<true>, dim3(grid), dim3(64), 0, s, ea, eb, 0, M, P, xu, goals, fext, active, lin,
-                          cost, qpd, init_active, st);
-  else
-    hipExtLaunchKernelGGL(i7m::k_linearize<false>, dim3(grid), dim3(64), 0, s, ea, eb, 0, M, P, xu, goals, fext, active, lin,
-                          cost, qpd, init_active, st);
+  auto go = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, s, ea, eb, 0, M, P, xu, goals, fext, active, lin, cost, qpd,
+                          init_active, st);
+  };
+  const bool fw = fext && fext_world;
+  if (spec && fw) go(i7m::k_linearize<true, true>);
+  else if (spec) go(i7m::k_linearize<true, false>);
+  else if (fw) go(i7m::k_linearize<false, true>);
+  else go(i7m::k_linearize<false, false>);
 }

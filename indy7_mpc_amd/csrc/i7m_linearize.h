@@ -61,7 +61,10 @@ __device__ __forceinline__ void imul(double m, const double* h, const double* I,
   o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
 }
 
-template <bool SPEC>
+// FW: the external wrench (fext, (B, 6) per problem) is a WORLD-frame spatial force about the
+// world origin (I7M_WRENCH_WORLD); otherwise it is constant in the joint-6 frame (pinocchio
+// f_ext, I7M_WRENCH_LOCAL).
+template <bool SPEC, bool FW = false>
 __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
                                                   const double* __restrict__ xu, const double* __restrict__ goals,
                                                   const double* __restrict__ fext, const int* __restrict__ active,
@@ -226,7 +229,12 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
     fcross(Vj, hV, VxH);
 #pragma unroll
     for (int r = 0; r < 6; ++r) F0[r] = IA[r] + VxH[r];
-    if (fext && j == 5 && valid) {
+    if (FW && fext && j == 5 && valid) {
+      // a world-frame wrench acts on link 6 as it is
+      const double* fe = fext + 6L * b;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) F0[r] -= fe[r];
+    } else if (fext && j == 5 && valid) {
       // local joint-6 wrench -> world: f_w = R f, n_w = R n + p x f_w
       const double* fe = fext + 6L * b;
       double fw[3], nw[3];
@@ -390,6 +398,19 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
       dq[r] = dot6(o + 12, yj);
       dv[r] = dot6(o + 12, zj);
     }
+  }
+  if (FW && fext && valid) {
+    // The formulas above differentiate forces that move with the bodies.  A world-frame wrench
+    // does not turn with the arm, so d tau_r / d q_j loses the term S_r . (S_j x* f_w) that a
+    // body-fixed one carries (tau_r = S_r . F^c_r; d(X* f)/dq_j = S_j x* (X* f)): add it back
+    // with the opposite sign of the subtracted wrench, i.e. +S_r . (S_j x* f_w).
+    const double* fe = fext + 6L * b;
+    double fw6[6], tS[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) fw6[r] = fe[r];
+    fcross(Sj, fw6, tS);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) dq[r] += dot6(&xs[gg][r][12], tS);
   }
   chol6_solve(L, dq);
   chol6_solve(L, dv);

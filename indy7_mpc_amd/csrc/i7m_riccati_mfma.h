@@ -1,6 +1,6 @@
 // i7m_riccati_mfma.h — the SQP subproblem QP solved with fp64 MFMA (v_mfma_f64_16x16x4), one
-// wavefront per problem.  Same math as k_riccati (i7m_riccati.h), reorganised for the matrix
-// cores (reference: the QP handed to OSQP at src/osqp_solver.py:137-143).
+// wavefront per problem: the exact solve of the equality-constrained QP the reference hands
+// OSQP (src/osqp_solver.py:137-143), a Riccati recursion laid out for the matrix cores.
 //
 // Homogeneous coordinates x~ = [x; 1] (13 states, padded to a 16x16 tile) fold the affine
 // dynamics offset c and every linear cost term into the matrix products:
@@ -21,7 +21,6 @@
 #endif
 
 #include "i7m_kernels.h"
-#include "i7m_riccati.h"
 
 namespace i7m {
 

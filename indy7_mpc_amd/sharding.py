@@ -61,4 +61,7 @@ class ShardedSQP:
         if errs:
             raise errs[0]
         parts = [o for o in outs if o is not None]
+        if not parts:  # B = 0: empty results, as Handle.solve / i7m_solve give
+            from ._lib import STATS_DTYPE
+            return np.empty((0, XU.shape[1] if XU.ndim == 2 else 18 * self.N - 6)), np.zeros(0, dtype=STATS_DTYPE)
         return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])

@@ -7,17 +7,21 @@ import os
 import numpy as np
 
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libi7m_cpu.so")
+# -march=native build for the host it is built on (bench.py builds it on the GPU box)
+LIB_NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libi7m_cpu_native.so")
 _DP = C.POINTER(C.c_double)
 _IP = C.POINTER(C.c_int)
 _lib = None
 
 
-def load():
+def load(path=None):
+    """dlopen the port (once; `path` selects a build, default the portable one)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            raise RuntimeError(f"{LIB} missing: run `make -C oracle/cpp`")
-        _lib = C.CDLL(LIB)
+        path = path or LIB
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle/cpp`")
+        _lib = C.CDLL(path)
         _lib.i7m_cpu_solve.argtypes = [_DP, C.c_int, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP, _DP, _DP,
                                        C.c_int]
         _lib.i7m_cpu_count_flops.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, C.c_int, _DP]

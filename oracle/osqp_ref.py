@@ -44,8 +44,12 @@ class OSQPSolverRef:
     """Restates OSQPSolver (src/osqp_solver.py:6-155); QP solved exactly."""
 
     def __init__(self, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
-                 qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30):
+                 qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30, fext6=None, fext_frame="local"):
         self.P_ = P or rbd.params()
+        # external wrench on joint 6 in every dynamics evaluation (batch_sqp's
+        # set_external_wrench_batch; frame "world": converted per configuration, rbd.fext_list)
+        self.fext6 = None if fext6 is None else np.asarray(fext6, float)
+        self.fext_frame = fext_frame
         self.N, self.dt = N, dt
         self.nq = self.nv = rbd.NJ
         self.nx = self.nq + self.nv
@@ -90,7 +94,7 @@ class OSQPSolverRef:
 
     # src/osqp_solver.py:70-81
     def compute_dynamics_jacobians(self, q, v, u):
-        d_dq, d_dv, d_du, a = rbd.aba_derivatives(q, v, u, self.P_)
+        d_dq, d_dv, d_du, a = rbd.aba_derivatives(q, v, u, self.P_, self.fext6, self.fext_frame)
         nx, nq = self.nx, self.nq
         self.A_k[nx + nq:, :nq] = d_dq * self.dt
         self.A_k[nx + nq:, nq:2 * nq] = d_dv * self.dt + np.eye(self.nv)
@@ -266,7 +270,7 @@ class SQPRef:
             q = XU[k * st: k * st + s.nq]
             v = XU[k * st + s.nq: k * st + s.nx]
             u = XU[k * st + s.nx: (k + 1) * st]
-            a = rbd.aba(q, v, u, s.P_)
+            a = rbd.aba(q, v, u, s.P_, rbd.fext_list(q, s.fext6, s.fext_frame, s.P_))
             qn = rbd.integrate(q, v * s.dt)
             vn = v + a * s.dt
             err += np.linalg.norm(qn - XU[(k + 1) * st: (k + 1) * st + s.nq]) + \

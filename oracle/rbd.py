@@ -244,22 +244,45 @@ def aba(q, v, tau, P: Params = None, fext=None):
     return qdd
 
 
-def aba_derivatives(q, v, tau, P: Params = None):
+def wrench_world_to_local(q, fw, P: Params = None):
+    """World-frame spatial force [f; n] (about the world origin) -> joint 6's local frame:
+    data.oMi[6].actInv(pin.Force(f, n)) at configuration q (src/gato_mpc_batch_sample.py:151-161),
+    f_l = R' f, n_l = R' (n - p x f).  Complex-step safe."""
+    R, p = fk(q, P)[-1]
+    fw = np.asarray(fw)
+    f, n = fw[:3], fw[3:]
+    return np.concatenate([R.T @ f, R.T @ (n - _cross(p, f))])
+
+
+def fext_list(q, fext6=None, frame="local", P: Params = None):
+    """pinocchio's f_ext vector (6 local spatial forces) for a wrench on joint 6 given in
+    `frame` ("local": as it is; "world": converted at q), or None."""
+    if fext6 is None:
+        return None
+    f = wrench_world_to_local(q, fext6, P) if frame == "world" else np.asarray(fext6)
+    return [np.zeros(6)] * (NJ - 1) + [f]
+
+
+def aba_derivatives(q, v, tau, P: Params = None, fext6=None, frame="local"):
     """pin.computeABADerivatives -> (da/dq, da/dv, da/dtau=Minv) and ddq.
 
-    Complex-step on RNEA at (q, v, a=ddq): exact to rounding."""
+    Complex-step on RNEA at (q, v, a=ddq): exact to rounding.  With a joint-6 wrench fext6
+    (frame "local" or "world", see fext_list) the derivatives include it; a world-frame wrench's
+    conversion to the local frame depends on q and is differentiated through."""
     P = P or params()
     M = crba(q, P)
     Minv = np.linalg.inv(M)
     Minv = 0.5 * (Minv + Minv.T)
-    a = aba(q, v, tau, P)
+    a = aba(q, v, tau, P, fext_list(q, fext6, frame, P))
     dtq = np.zeros((NJ, NJ))
     dtv = np.zeros((NJ, NJ))
+    fv = fext_list(q, fext6, frame, P)
     for j in range(NJ):
         e = np.zeros(NJ, dtype=complex)
         e[j] = 1j * H_CS
-        dtq[:, j] = np.imag(_rnea_impl(q + e, v.astype(complex), a.astype(complex), P, True, None)) / H_CS
-        dtv[:, j] = np.imag(_rnea_impl(q.astype(complex), v + e, a.astype(complex), P, True, None)) / H_CS
+        fq = fext_list(q + e, fext6, frame, P)
+        dtq[:, j] = np.imag(_rnea_impl(q + e, v.astype(complex), a.astype(complex), P, True, fq)) / H_CS
+        dtv[:, j] = np.imag(_rnea_impl(q.astype(complex), v + e, a.astype(complex), P, True, fv)) / H_CS
     return -Minv @ dtq, -Minv @ dtv, Minv, a
 
 
@@ -268,8 +291,12 @@ def integrate(q, dq):
     return q + dq
 
 
-def rk4(q, v, u, dt, fext=None, P: Params = None):
-    """Plant integrator restating src/utils.py:3-18 (4 x pin.aba with optional f_ext)."""
+def rk4(q, v, u, dt, fext=None, P: Params = None, fext6_world=None):
+    """Plant integrator restating src/utils.py:3-18 (4 x pin.aba with optional f_ext).
+    fext6_world: a world-frame joint-6 wrench, converted ONCE at the start q and held over the
+    four stages, as the reference's host plant does (src/gato_mpc_batch_sample.py:270-279)."""
+    if fext6_world is not None:
+        fext = fext_list(q, fext6_world, "world", P)
     k1q = v
     k1v = aba(q, v, u, P, fext)
     q2 = integrate(q, k1q * dt / 2)

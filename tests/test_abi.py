@@ -92,3 +92,15 @@ def test_no_cpu_fallback_without_gpu(lib, model):
 
     with pytest.raises(_lib.I7MError):
         OSQPSolver(model, N=16)
+
+
+def test_version_is_stamped_with_the_source_tree(lib):
+    """i7m_version() carries the sha256 prefix of the sources it was built from
+    (__graft_entry__.src_hash): the loaded binary matches this tree, and it is the release
+    build (no I7M_DIAG ablation kernels)."""
+    from indy7_mpc_amd import _lib
+    import __graft_entry__ as ge
+
+    v = _lib.version()
+    assert v.endswith("src " + ge.src_hash()), (v, ge.src_hash())
+    assert "release" in v

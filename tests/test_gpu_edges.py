@@ -120,6 +120,9 @@ def test_device_solve_out_of_place(lib, model, graph, monkeypatch):
     t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
     t_out = torch.full_like(t_xu, float("nan"))
     t_st = torch.zeros(B * lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    # torch filled the buffers on its current stream: order the solve after it;
+    # the default stream is the null stream (0), which the handle's own blocking stream follows
+    h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     for _ in range(3):
         h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
         torch.cuda.synchronize(dev)
@@ -147,3 +150,26 @@ def test_linesearch_one_and_four_waves_agree(lib, model, N, monkeypatch):
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1]["alphas"], outs[1][1]["alphas"])
     _check_sqp(outs[1][0], outs[1][1], xcur, goals, XU, N=N)
+
+
+def test_release_library_refuses_ablation_knob(lib, model, monkeypatch):
+    """I7M_ABLATE selects invalid-result timing kernels that exist only in the -DI7M_DIAG build:
+    the shipping library refuses to create a handle while it is set (no silent wrong answers)."""
+    assert "release" in lib.version()
+    monkeypatch.setenv("I7M_ABLATE", "4")
+    with pytest.raises(lib.I7MError, match="I7M_ABLATE"):
+        lib.Handle(model, N=16)
+    monkeypatch.delenv("I7M_ABLATE")
+    lib.Handle(model, N=16).close()
+
+
+def test_zero_step_accepts_alpha_one(lib, model):
+    """A QP minimiser equal to XU (sol == XU): the reference's merit_new == basemerit exactly, so
+    alpha = 1 is accepted (src/osqp_sqp.py:58-72).  The line-search hook (base evaluated by the
+    candidate function) must agree."""
+    N, B = 16, 3
+    xcur, goals, XU = synthetic_batch(B, N, seed=19)
+    XU = XU + np.random.default_rng(3).normal(0, 0.2, XU.shape)
+    h = lib.Handle(model, N=N, max_batch=B)
+    al = h.linesearch(XU, XU, goals)
+    np.testing.assert_array_equal(al, np.ones(B))

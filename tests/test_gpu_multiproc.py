@@ -1,0 +1,26 @@
+"""GPU: the multi-rank sharded path for real — several processes, each with its own library
+handle on the one GPU, solving contiguous shards (sharding.shard_range, as bench.py's ranks do);
+their concatenated outputs must equal the single-process solve bit for bit.
+
+The ranks are spawned by a fresh child process (tools/shard_ranks.py) that has not touched the
+GPU, so no GPU-initialised process forks ranks.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world,batch", [(2, 96), (3, 50)])
+def test_ranks_on_shards_equal_single_process(world, batch):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "shard_ranks.py"), "--world", str(world),
+                        "--batch", str(batch)], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["equal"] and len(res["ranges"]) == world
+    assert res["ranges"][0][0] == 0 and res["ranges"][-1][1] == batch

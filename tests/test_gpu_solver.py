@@ -182,57 +182,6 @@ def test_goal_stride_6_equals_stride_3(lib, model):
     np.testing.assert_array_equal(o3, o6)
 
 
-def test_batch_sqp_surface_with_wrench(lib, model):
-    from indy7_mpc_amd.bindings import batch_sqp
-
-    N, B = 16, 4
-    xcur, goals, XU = synthetic_batch(B, N, seed=13)
-    g6 = np.zeros((B, 6 * N))
-    for k in range(N):
-        g6[:, 6 * k:6 * k + 3] = goals[:, 3 * k:3 * k + 3]
-    s = batch_sqp.SQPSolverfloat_4()
-    f = np.zeros((B, 6))
-    f[1:, :3] = np.random.default_rng(1).normal(0, 5, (B - 1, 3))
-    s.set_external_wrench_batch(f)
-    s.reset(); s.resetRho(); s.resetLambda()
-    r = s.solve(XU, 0.01, xcur, g6)
-    assert set(r) == {"xu_trajectory", "solve_time_us", "sqp_iterations", "pcg_stats", "line_search_stats"}
-    assert r["xu_trajectory"].shape == (B, 18 * N - 6)
-    # problem 0 has no wrench -> equals the plain solver
-    h = lib.Handle(model, N=N, max_batch=B)
-    plain, _ = h.solve(xcur, goals, XU)
-    np.testing.assert_array_equal(r["xu_trajectory"][0], plain[0])
-    assert not np.array_equal(r["xu_trajectory"][1], plain[1])
-    # sim_forward: one rk4 step per wrench hypothesis, vs the oracle
-    xn = s.sim_forward(xcur[0], np.full(6, 2.0), 0.01)
-    for b in range(B):
-        q, v = rbd.rk4(xcur[0][:6], xcur[0][6:], np.full(6, 2.0), 0.01, fext=[np.zeros(6)] * 5 + [f[b]])
-        np.testing.assert_allclose(xn[b], np.concatenate([q, v]), rtol=1e-10, atol=1e-12)
-
-
-def test_wrench_solve_matches_oracle_dynamics(lib, model):
-    """Linearisation with a local joint-6 wrench == oracle ABA derivatives with f_ext."""
-    N = 16
-    xcur, goals, XU = synthetic_batch(1, N, seed=14)
-    XU = XU + np.random.default_rng(2).normal(0, 0.2, XU.shape)
-    fw = np.array([[3.0, -4.0, 5.0, 0.1, 0.2, -0.3]])
-    h = lib.Handle(model, N=N, max_batch=1)
-    h.set_external_wrench(fw)
-    lin, _ = h.linearize(XU, goals)
-    fext = [np.zeros(6)] * 5 + [fw[0]]
-    for k in (0, 7, N - 2):
-        q, v, u = XU[0][18 * k:18 * k + 6], XU[0][18 * k + 6:18 * k + 12], XU[0][18 * k + 12:18 * k + 18]
-        a = rbd.aba(q, v, u, fext=fext)
-        np.testing.assert_allclose(lin[0, k, 108:], a, rtol=1e-10, atol=1e-9)
-        # complex-step derivative of the wrench-loaded RNEA
-        M = rbd.crba(q)
-        dtq = np.array([np.imag(rbd.rnea(q + 1e-30j * e, v.astype(complex), a.astype(complex), fext=fext)) / 1e-30
-                        for e in np.eye(6)]).T
-        dq = -np.linalg.solve(M, dtq)
-        np.testing.assert_allclose(lin[0, k, :36].reshape(6, 6), 0.01 * dq, rtol=1e-9, atol=1e-11)
-    h.set_external_wrench(None)
-
-
 def test_sharded_solver_matches_single(lib, model):
     from indy7_mpc_amd.sharding import ShardedSQP
 

@@ -1,0 +1,164 @@
+"""GPU: the external wrench on joint 6 (batch_sqp.set_external_wrench_batch, gato_controller.py:
+77-90,120-129) in both frames, through the C-ABI, against the oracle.
+
+  * I7M_WRENCH_WORLD (batch_sqp's default): a world-frame spatial force [f; n] about the world
+    origin, converted to joint 6's frame at each configuration with oMi[6].actInv as the
+    reference's host code does (src/gato_mpc_batch_sample.py:151-161,270-279).  The oracle
+    (rbd.fext_list / rbd.aba_derivatives(frame="world")) differentiates that conversion by
+    complex step, so the linearisation is checked including the conversion's q-dependence.
+  * I7M_WRENCH_LOCAL: constant in joint 6's frame (pinocchio f_ext as it is).
+
+GATO (the reference's batch_sqp) is absent, so the solver side of this is parity-unpinned against
+the reference; the frame convention is pinned by the reference's own host plant.
+
+Tolerances (fp64): dynamics and derivatives 1e-9 relative to the array's max (complex-step
+oracle); rk4 / merit 1e-10 relative; full SQP 1e-6 relative with the alpha sequence identical.
+"""
+import numpy as np
+import pytest
+
+from oracle import rbd
+from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+DT = 0.01
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def _knot(XU, k):
+    return XU[18 * k:18 * k + 6], XU[18 * k + 6:18 * k + 12], XU[18 * k + 12:18 * k + 18]
+
+
+def _close(got, ref, tol):
+    assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (np.abs(got - ref).max(), np.abs(ref).max())
+
+
+@pytest.mark.parametrize("frame", ["local", "world"])
+def test_wrench_linearisation_matches_oracle(lib, model, frame):
+    """k_linearize with a joint-6 wrench == complex-step ABA derivatives of the wrench-loaded
+    dynamics (for "world" including d(actInv(oMi6(q)) f)/dq)."""
+    N = 16
+    xcur, goals, XU = synthetic_batch(2, N, seed=14)
+    XU = XU + np.random.default_rng(2).normal(0, 0.3, XU.shape)
+    fw = np.array([[3.0, -4.0, 5.0, 0.1, 0.2, -0.3], [-20.0, 10.0, 40.0, 0.0, 0.0, 0.0]])
+    h = lib.Handle(model, N=N, max_batch=2)
+    h.set_external_wrench(fw, frame)
+    lin, _ = h.linearize(XU, goals)
+    for b in range(2):
+        for k in (0, 7, N - 2):
+            q, v, u = _knot(XU[b], k)
+            dq, dv, Mi, a = rbd.aba_derivatives(q, v, u, fext6=fw[b], frame=frame)
+            _close(lin[b, k, 108:], a, 1e-10)
+            _close(lin[b, k, :36].reshape(6, 6), DT * dq, 1e-9)
+            _close(lin[b, k, 36:72].reshape(6, 6), np.eye(6) + DT * dv, 1e-9)
+            _close(lin[b, k, 72:108].reshape(6, 6), DT * Mi, 1e-9)
+    h.set_external_wrench(None)
+    lin0, _ = h.linearize(XU, goals)
+    assert not np.allclose(lin0, lin)
+
+
+def test_world_wrench_aba_rk4_merit_match_oracle(lib, model):
+    rng = np.random.default_rng(5)
+    n = 7
+    q = rng.uniform(-2, 2, (n, 6))
+    v = rng.uniform(-1, 1, (n, 6))
+    u = rng.uniform(-20, 20, (n, 6))
+    fw = np.hstack([rng.normal(0, 30, (n, 3)), rng.normal(0, 2, (n, 3))])
+    h = lib.Handle(model, N=16, max_batch=8)
+    a = h.aba(q, v, u, fext=fw, frame="world")
+    qo, vo = h.rk4(q, v, u, DT, fext=fw, frame="world")
+    for i in range(n):
+        _close(a[i], rbd.aba(q[i], v[i], u[i], fext=rbd.fext_list(q[i], fw[i], "world")), 1e-10)
+        rq, rv = rbd.rk4(q[i], v[i], u[i], DT, fext6_world=fw[i])
+        _close(qo[i], rq, 1e-12)
+        _close(vo[i], rv, 1e-10)
+    # local frame is a different model: same numbers only where the conversion is the identity
+    al = h.aba(q, v, u, fext=fw, frame="local")
+    assert not np.allclose(al, a)
+    # merit pieces with a world wrench (the line search's integrator error)
+    N = 16
+    xcur, goals, XU = synthetic_batch(2, N, seed=6)
+    XU = XU + rng.normal(0, 0.2, XU.shape)
+    h.set_external_wrench(fw[:2], "world")
+    m = h.merit(XU, XU, goals)
+    for b in range(2):
+        sq = SQPRef(OSQPSolverRef(N=N, fext6=fw[b], fext_frame="world"))
+        ie = sq.integrator_err(XU[b])
+        assert abs(m[b, 3] - ie) <= 1e-10 * ie
+
+
+@pytest.mark.parametrize("frame", ["world", "local"])
+def test_wrench_full_sqp_matches_oracle(lib, model, frame):
+    """Whole SQP solves with a per-problem joint-6 wrench == the oracle SQP with the same wrench
+    and frame (alpha sequence identical)."""
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, seed=13)
+    f = np.zeros((B, 6))
+    f[1:, :3] = np.random.default_rng(1).normal(0, 15, (B - 1, 3))  # forces only, as the callers draw them
+    f[3, 3:] = [0.5, -0.5, 1.0]
+    h = lib.Handle(model, N=N, max_batch=B)
+    h.set_external_wrench(f, frame)
+    out, st = h.solve(xcur, goals, XU)
+    for b in range(B):
+        sq = SQPRef(OSQPSolverRef(N=N, fext6=f[b], fext_frame=frame))
+        ref = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        s = sq.get_stats()
+        assert st["qp_iters"][b] == s["qp_iters"]["values"][0]
+        np.testing.assert_array_equal(st["alphas"][b][:st["n_alphas"][b]], s["linesearch_alphas"]["values"])
+        assert np.linalg.norm(out[b] - ref) / np.linalg.norm(ref) < 1e-6
+    # problem 0 carries no wrench: the plain solver's answer, bit for bit
+    h0 = lib.Handle(model, N=N, max_batch=B)
+    plain, _ = h0.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(out[0], plain[0])
+    assert not np.array_equal(out[1], plain[1])
+
+
+def test_batch_sqp_surface_world_wrench(lib, model):
+    """bindings.batch_sqp as gato_controller.py drives it: world-frame force hypotheses
+    (torque part zero, row 0 zero, gato_controller.py:77-81), solve, sim_forward per hypothesis
+    against the reference's host plant (actInv at x, then rk4), and find_best_idx picks the
+    hypothesis that generated the measured state (gato_controller.py:109-118)."""
+    from indy7_mpc_amd.bindings import batch_sqp
+
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, seed=13)
+    g6 = np.zeros((B, 6 * N))
+    for k in range(N):
+        g6[:, 6 * k:6 * k + 3] = goals[:, 3 * k:3 * k + 3]
+    f = np.random.default_rng(1).normal(0, 30, (B, 6))
+    f[:, 3:] = 0.0
+    f[0] = 0.0
+    s = batch_sqp.SQPSolverfloat_4()
+    assert s.wrench_frame == "world"
+    s.set_external_wrench_batch(f)
+    s.reset(); s.resetRho(); s.resetLambda()
+    r = s.solve(XU, DT, xcur, g6)
+    assert set(r) == {"xu_trajectory", "solve_time_us", "sqp_iterations", "pcg_stats", "line_search_stats"}
+    h = lib.Handle(model, N=N, max_batch=B)
+    h.set_external_wrench(f, "world")
+    ref, _ = h.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(r["xu_trajectory"], ref)
+    # sim_forward: one rk4 step per hypothesis, the world force converted at x (the host plant)
+    u = np.full(6, 2.0)
+    xn = s.sim_forward(xcur[0], u, DT)
+    for b in range(B):
+        q, v = rbd.rk4(xcur[0][:6], xcur[0][6:], u, DT, fext6_world=f[b])
+        np.testing.assert_allclose(xn[b], np.concatenate([q, v]), rtol=1e-10, atol=1e-12)
+    # find_best_idx: the measured next state came from hypothesis 2's force
+    q, v = rbd.rk4(xcur[0][:6], xcur[0][6:], u, DT, fext6_world=f[2])
+    meas = np.concatenate([q, v])
+    assert int(np.argmin(np.linalg.norm(xn - meas, axis=1))) == 2
+    # the local-frame option is the other model
+    sl = batch_sqp.SQPSolverfloat_4(wrench_frame="local")
+    sl.set_external_wrench_batch(f)
+    rl = sl.solve(XU, DT, xcur, g6)
+    np.testing.assert_array_equal(rl["xu_trajectory"][0], ref[0])
+    assert not np.array_equal(rl["xu_trajectory"][1], ref[1])
