@@ -114,10 +114,11 @@ def test_wrench_full_sqp_matches_oracle(lib, model, frame):
         assert st["qp_iters"][b] == s["qp_iters"]["values"][0]
         np.testing.assert_array_equal(st["alphas"][b][:st["n_alphas"][b]], s["linesearch_alphas"]["values"])
         assert np.linalg.norm(out[b] - ref) / np.linalg.norm(ref) < 1e-6
-    # problem 0 carries no wrench: the plain solver's answer, bit for bit
+    # problem 0 carries no wrench: the plain solver's answer (to rounding: the wrench-carrying
+    # kernel instances are compiled separately, so their FMA contraction may differ)
     h0 = lib.Handle(model, N=N, max_batch=B)
     plain, _ = h0.solve(xcur, goals, XU)
-    np.testing.assert_array_equal(out[0], plain[0])
+    assert np.linalg.norm(out[0] - plain[0]) <= 1e-12 * np.linalg.norm(plain[0])
     assert not np.array_equal(out[1], plain[1])
 
 
@@ -160,5 +161,5 @@ def test_batch_sqp_surface_world_wrench(lib, model):
     sl = batch_sqp.SQPSolverfloat_4(wrench_frame="local")
     sl.set_external_wrench_batch(f)
     rl = sl.solve(XU, DT, xcur, g6)
-    np.testing.assert_array_equal(rl["xu_trajectory"][0], ref[0])
+    assert np.linalg.norm(rl["xu_trajectory"][0] - ref[0]) <= 1e-12 * np.linalg.norm(ref[0])
     assert not np.array_equal(rl["xu_trajectory"][1], ref[1])

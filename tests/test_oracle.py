@@ -81,6 +81,43 @@ def test_fext_consistency():
     np.testing.assert_allclose(rbd.rnea(q, v, a, fext=f), t, atol=1e-9)
 
 
+def test_world_wrench_oracle():
+    """World-frame joint-6 wrench (gato_controller.py:77-81 draws them; the reference converts
+    with oMi[6].actInv, src/gato_mpc_batch_sample.py:151-161):
+      * the conversion is pinocchio's actInv: the converted local force, moved back to the
+        world origin by oMi[6], is the world force again;
+      * the complex-step derivatives of the world-wrench dynamics match central differences of
+        ABA with the wrench re-converted at every perturbed q;
+      * rk4 with a world wrench converts once at the start q (the host plant, :270-279)."""
+    rng = np.random.default_rng(11)
+    q, v, t = rng.uniform(-2, 2, 6), rng.uniform(-1, 1, 6), rng.uniform(-30, 30, 6)
+    fw = np.concatenate([rng.normal(0, 30, 3), rng.normal(0, 3, 3)])
+    R, p = rbd.fk(q)[-1]
+    fl = rbd.wrench_world_to_local(q, fw)
+    f_back = R @ fl[:3]
+    np.testing.assert_allclose(f_back, fw[:3], atol=1e-12)
+    np.testing.assert_allclose(R @ fl[3:] + np.cross(p, f_back), fw[3:], atol=1e-12)
+    dq, dv, Mi, a = rbd.aba_derivatives(q, v, t, fext6=fw, frame="world")
+    np.testing.assert_allclose(a, rbd.aba(q, v, t, fext=rbd.fext_list(q, fw, "world")), rtol=1e-12)
+    h = 1e-6
+
+    def aw(qq, vv):
+        return rbd.aba(qq, vv, t, fext=rbd.fext_list(qq, fw, "world"))
+
+    fdq = np.array([(aw(q + h * e, v) - aw(q - h * e, v)) / (2 * h) for e in np.eye(6)]).T
+    fdv = np.array([(aw(q, v + h * e) - aw(q, v - h * e)) / (2 * h) for e in np.eye(6)]).T
+    assert np.abs(fdq - dq).max() <= 1e-5 * max(1, np.abs(dq).max())
+    assert np.abs(fdv - dv).max() <= 1e-5 * max(1, np.abs(dv).max())
+    # a local-frame wrench of the same value at q gives the same a but different d/dq
+    dql, _, _, al = rbd.aba_derivatives(q, v, t, fext6=fl, frame="local")
+    np.testing.assert_allclose(al, a, rtol=1e-10)
+    assert np.abs(dql - dq).max() > 1e-3 * np.abs(dq).max()
+    qw, vw = rbd.rk4(q, v, t, 0.01, fext6_world=fw)
+    ql, vl = rbd.rk4(q, v, t, 0.01, fext=[np.zeros(6)] * 5 + [fl])
+    np.testing.assert_array_equal(qw, ql)
+    np.testing.assert_array_equal(vw, vl)
+
+
 @pytest.mark.parametrize("N", [16, 32, 64])
 def test_csc_templates(N):
     s = OSQPSolverRef(N=N)
