@@ -46,7 +46,7 @@ def _qp_inputs(N, B, seed=46):
     return np.vstack([xcur, xcur]), np.vstack([goals, goals]), np.vstack([XU, XU2])
 
 
-@pytest.mark.parametrize("N,ipm", [(16, None), (32, None), (32, "split"), (32, "delta")])
+@pytest.mark.parametrize("N,ipm", [(16, None), (32, None), (64, None), (32, "split"), (32, "delta")])
 def test_box_qp_matches_oracle(lib, model, N, ipm, monkeypatch):
     """Default k_ipm_fused, and the split-launch and factorisation-reuse (delta) variants."""
     if ipm:
@@ -104,3 +104,12 @@ def test_config4_full_size(lib, model):
     assert (out[:, bm] >= lo[bm]).all() and (out[:, bm] <= hi[bm]).all()
     assert conv.mean() >= 0.99, conv.mean()
     np.testing.assert_array_equal(out[:, :12], xcur)
+    # two problems of the full-size batch against the oracle SQP with box rows (config 4's exact
+    # size meets its oracle: same alpha sequence, 1e-5 relative)
+    s = OSQPSolverRef(N=N, qp="box")
+    for b in np.random.default_rng(4).choice(B, 2, replace=False):
+        sq = SQPRef(s)
+        ref = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        al = list(st["alphas"][b][: st["n_alphas"][b]])
+        assert al == sq.stats["linesearch_alphas"]["values"], (b, al, sq.stats["linesearch_alphas"]["values"])
+        assert _relerr(out[b], ref) <= 1e-5, (b, _relerr(out[b], ref))
