@@ -62,6 +62,11 @@ extern "C" {
 #define I7M_ENODEV -4   /* no usable gfx950 device */
 
 enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1 };
+/* How a solve is launched (I7M_QP_DIRECT): FUSED = one kernel per solve (a workgroup per
+ * problem runs every SQP iteration's linearisation, QP and line search), FUSED_ITER = that kernel
+ * once per SQP iteration, SPLIT = three kernels per SQP iteration; AUTO picks by batch size
+ * (DESIGN.md §4.5).  Bit-identical results in every mode. */
+enum { I7M_PIPE_AUTO = 0, I7M_PIPE_SPLIT = 1, I7M_PIPE_FUSED = 2, I7M_PIPE_FUSED_ITER = 3 };
 #define I7M_BOX_Q 1     /* q_lower <= q <= q_upper    description/indy7.urdf:203-238 <limit> */
 #define I7M_BOX_V 2     /* |v| <= velocity limit */
 #define I7M_BOX_U 4     /* |u| <= effort limit */
@@ -97,6 +102,8 @@ typedef struct i7m_config {
   int32_t box_mask;     /* which rows: I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U (default all) */
   int32_t box_max_iters;/* interior-point iterations per QP, default 30 */
   double box_tol;       /* stop when mu < tol and the residuals shrank by tol, default 1e-8 */
+  int32_t pipeline;     /* I7M_PIPE_* (appended), default I7M_PIPE_AUTO */
+  int32_t pad;
 } i7m_config;
 
 /* Per-problem SQP statistics (keys of SQP_OSQP.stats, src/osqp_sqp.py:7-11). */
@@ -186,7 +193,7 @@ int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,
-       I7M_K_COUNT = 6 };
+       I7M_K_SQP_FUSED = 6, I7M_K_COUNT = 7 };
 int i7m_set_timing(i7m_handle* h, int enable);
 /* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
 int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);

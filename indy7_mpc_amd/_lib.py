@@ -25,8 +25,9 @@ MAX_SQP = 8
 MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
-I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_COUNT = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused")
+I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_SQP_FUSED = range(7)
+I7M_K_COUNT = 7
+KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused", "k_sqp_fused")
 
 
 class I7MError(RuntimeError):
@@ -67,10 +68,13 @@ class i7m_config(C.Structure):
         ("box_mask", C.c_int32),
         ("box_max_iters", C.c_int32),
         ("box_tol", C.c_double),
+        ("pipeline", C.c_int32),
+        ("pad", C.c_int32),
     ]
 
 
 QP_DIRECT, QP_BOX = 0, 1
+PIPE_AUTO, PIPE_SPLIT, PIPE_FUSED, PIPE_FUSED_ITER = 0, 1, 2, 3
 WRENCH_LOCAL, WRENCH_WORLD = 0, 1
 _FRAMES = {"local": WRENCH_LOCAL, "world": WRENCH_WORLD, WRENCH_LOCAL: WRENCH_LOCAL, WRENCH_WORLD: WRENCH_WORLD}
 BOX_Q, BOX_V, BOX_U = 1, 2, 4
@@ -184,7 +188,7 @@ class Handle:
 
     def __init__(self, model, N=32, dt=0.01, dQ_cost=0.01, R_cost=1e-5, QN_cost=100.0, regularize=True, eps=1.0,
                  max_batch=1, device_id=0, mu=10.0, step_tol=1e-3, max_sqp_iters=2, qp_mode=QP_DIRECT,
-                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8):
+                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8, pipeline=PIPE_AUTO):
         lib = load()
         cfg = i7m_config()
         _check(lib.i7m_config_default(C.byref(cfg)))
@@ -192,6 +196,7 @@ class Handle:
         cfg.regularize, cfg.eps, cfg.mu, cfg.step_tol = int(bool(regularize)), float(eps), float(mu), float(step_tol)
         cfg.max_sqp_iters, cfg.max_batch, cfg.device_id = int(max_sqp_iters), int(max_batch), int(device_id)
         cfg.qp_mode, cfg.box_mask, cfg.box_max_iters, cfg.box_tol = int(qp_mode), int(box_mask), int(box_max_iters), float(box_tol)
+        cfg.pipeline = int(pipeline)
         packed = np.ascontiguousarray(model.packed(), dtype=np.float64)
         assert packed.nbytes == C.sizeof(i7m_model), (packed.nbytes, C.sizeof(i7m_model))
         C.memmove(C.byref(cfg.model), packed.ctypes.data, packed.nbytes)

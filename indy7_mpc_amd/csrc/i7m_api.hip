@@ -40,6 +40,12 @@ void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t 
                                  bool fext_world, const int* active, double* lin, double* cost, double* qpd,
                                  int* init_active, void* init_stats);
 
+// i7m_fused_tu.hip (k_sqp_fused in a unit of its own)
+hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipStream_t s, hipEvent_t ea, hipEvent_t eb,
+                                const void* model, const void* params, const double* xu_in, double* xu_out,
+                                const double* xs, const double* goals, const double* fext, double* lin, double* cost,
+                                double* qpd, double* kbuf, double* sol, int* active, void* stats);
+
 static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
 
 namespace {
@@ -102,6 +108,7 @@ struct i7m_handle {
   bool use_graph = false;  // I7M_GRAPH=1: capture the solve once per buffer set, replay it
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
   int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
+  int pipeline = I7M_PIPE_AUTO;  // cfg.pipeline, or I7M_PIPE=split|fused
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -274,6 +281,9 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
   });
 }
 
+// waves per problem of the line search (k_linesearch) and of k_sqp_fused
+int waves_for(const i7m_handle* h, int B) { return h->ls_waves > 0 ? h->ls_waves : (B <= 256 ? 4 : 1); }
+
 // base_from_lin: lin/cost of W hold the linearisation of this xu (the SQP loop), so the base
 // merit comes from them (k_linesearch); otherwise candidate 0 is evaluated.
 // xu: the linearisation point; xu_out: where the updated XU goes (may be xu itself).
@@ -282,7 +292,7 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
                       double* alpha_out, int iter, int mode, bool base_from_lin) {
   if (P.B == 0) return I7M_OK;
   // small batches leave most SIMDs idle: spend them on evaluating every candidate in one round
-  const int nw = h->ls_waves > 0 ? h->ls_waves : (P.B <= 256 ? 4 : 1);
+  const int nw = waves_for(h, P.B);
   const size_t lds = ls_lds_bytes(P.T, nw);
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
@@ -369,6 +379,36 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   return I7M_OK;
 }
 
+// Does this solve run as one k_sqp_fused launch?  (Direct QP only; the box mode's interior point
+// has its own fused kernel between the Riccati and the line search.)  AUTO picks by batch size:
+// DESIGN.md §4.5 has the measurements behind the threshold.
+constexpr int FUSED_AUTO_MAX_B = 0;
+bool use_fused(const i7m_handle* h, int B) {
+  if (h->cfg.qp_mode != I7M_QP_DIRECT) return false;
+  if (h->pipeline == I7M_PIPE_FUSED || h->pipeline == I7M_PIPE_FUSED_ITER) return true;
+  if (h->pipeline == I7M_PIPE_SPLIT) return false;
+  return B <= FUSED_AUTO_MAX_B;
+}
+
+
+int launch_fused(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu_in, double* xu_out,
+                 const double* xs, const double* goals, ProblemStats* st) {
+  const int nw = waves_for(h, P.B);
+  // I7M_PIPE_FUSED_ITER: one launch per SQP iteration, else one per solve
+  const int launches = h->pipeline == I7M_PIPE_FUSED_ITER ? h->cfg.max_sqp_iters : 1;
+  for (int i = 0; i < launches; ++i) {
+    hipError_t e = hipSuccess;
+    const int rc = timed(h, s, I7M_K_SQP_FUSED, [&](hipEvent_t ea, hipEvent_t eb) {
+      e = i7m_launch_sqp_fused(h->spec, nw, h->fext_frame == I7M_WRENCH_WORLD, launches > 1 ? i : -1, s, ea, eb, h->d_model,
+                               &P, i == 0 ? xu_in : xu_out, xu_out, xs, goals, W.fext, W.lin, W.cost, W.qpd, W.kbuf,
+                               h->d_sol, h->d_active, st);
+    });
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(I7M_EHIP, std::string("k_sqp_fused launch: ") + hipGetErrorString(e));
+  }
+  return I7M_OK;
+}
+
 // The SQP loop on device buffers: iteration 1 reads xu_in and its line search writes every
 // row of xu_out; later iterations update xu_out in place (xu_in == xu_out is allowed).  The
 // first linearisation also initialises the active flags and the stats (no memset launches).
@@ -379,6 +419,7 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
   const Bufs W = bufs_at(h, 0);
   const SolveParams P = params_of(h, B, goal_stride);
   hipStream_t s = h->stream;
+  if (use_fused(h, B)) return launch_fused(h, s, W, P, d_xu_in, d_xu, d_xs, d_goals, d_st);
   for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
     const double* xin = it == 0 ? d_xu_in : d_xu;
     int rc;
@@ -504,6 +545,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (cfg->max_batch < 1) return fail(I7M_EINVAL, "max_batch must be >= 1");
   if (cfg->max_sqp_iters < 1 || cfg->max_sqp_iters > I7M_MAX_SQP) return fail(I7M_EINVAL, "max_sqp_iters in [1, 8]");
   if (cfg->qp_mode != I7M_QP_DIRECT && cfg->qp_mode != I7M_QP_BOX) return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (cfg->pipeline < I7M_PIPE_AUTO || cfg->pipeline > I7M_PIPE_FUSED_ITER) return fail(I7M_EINVAL, "unsupported pipeline");
   if (cfg->qp_mode == I7M_QP_BOX) {
     if (cfg->box_mask < 0 || cfg->box_mask > 7) return fail(I7M_EINVAL, "box_mask must be a subset of Q|V|U (0..7)");
     if (cfg->box_max_iters < 1 || cfg->box_max_iters > 200) return fail(I7M_EINVAL, "box_max_iters in [1, 200]");
@@ -544,6 +586,12 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
+  h->pipeline = cfg->pipeline;
+  if (const char* e = std::getenv("I7M_PIPE"))
+    h->pipeline = std::strcmp(e, "fused") == 0 ? I7M_PIPE_FUSED
+                   : std::strcmp(e, "fused_iter") == 0 ? I7M_PIPE_FUSED_ITER
+                   : std::strcmp(e, "split") == 0 ? I7M_PIPE_SPLIT
+                   : h->pipeline;
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
   // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
   const size_t scratch = std::max(Bm * T, (size_t)256 * 114);

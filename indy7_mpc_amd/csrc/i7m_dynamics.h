@@ -28,6 +28,30 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The same ordering among the lanes of ONE wavefront, for device bodies whose LDS region only
+// their own wave touches (the linearisation's per-knot exchanges, the Riccati recursion): the
+// fences of lds_sync() without the s_barrier.  In a single-wave workgroup this is exactly what
+// lds_sync() compiles to; in a multi-wave workgroup (k_sqp_fused) the other waves need not
+// take part.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// ... and for global memory too (a lane reads what another lane of the wave stored): the
+// __syncthreads() of a single-wave workgroup, without the barrier.
+__device__ __forceinline__ void wave_sync_all() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// Between the phases of k_sqp_fused: every wave's global stores complete and become visible to
+// every wave of the workgroup, L1 lines read before the phase are dropped (agent-scope acquire:
+// the next phase re-reads buffers an earlier phase cached and this one overwrote), then barrier.
+__device__ __forceinline__ void block_sync_global() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 // Device-side model: URDF numbers plus precomputed inertia about each joint origin.
 struct DevModel {
   double Rp[6][9];   // row-major

@@ -229,19 +229,18 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
 // candidate slots c0 + w R .. c0 + w R + R - 1 of each round, so W R candidates per round (all
 // eight alphas in one round at N = 32, W = 4).  Same first-accept rule, same merits.
 // FW: fext is a world-frame wrench (I7M_WRENCH_WORLD), see ls_merit_terms.
+// The line search of problem b by the W waves of a workgroup (wave w, lane l): the body of
+// k_linesearch, and the third phase of each SQP iteration of k_sqp_fused.  ls_dyn: the dynamic
+// LDS of ls_lds_bytes(T, W); merit: 9 doubles of LDS.
 template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
-                                                   const double* xu, double* xu_out, const double* __restrict__ sol,
-                                                   const double* __restrict__ goals, const double* __restrict__ fext,
-                                                   int* __restrict__ active,
-                                                   ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
-                                                   int iter, int mode, const double* __restrict__ lin = nullptr,
-                                                   const double* __restrict__ cost = nullptr) {
-  const int b = blockIdx.x;
-  if (b >= P.B) return;
-  if (active && !active[b]) return;
-  const int l = threadIdx.x & 63;
-  const int w = W > 1 ? (int)(threadIdx.x >> 6) : 0;
+__device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg, const SolveParams& P, const int b,
+                                                const int w, const int l, double* __restrict__ ls_dyn,
+                                                double* __restrict__ merit, const double* xu, double* xu_out,
+                                                const double* __restrict__ sol, const double* __restrict__ goals,
+                                                const double* __restrict__ fext, int* __restrict__ active,
+                                                ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
+                                                int iter, int mode, const double* __restrict__ lin,
+                                                const double* __restrict__ cost) {
   const int N = P.N;
   const int R = (N >= 64) ? 1 : 64 / N;
   const int slot = l / N;
@@ -253,17 +252,15 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
   // the problem's XU and QP minimiser, staged once in LDS for every round
   // dynamic LDS (ls_lds_bytes): (XU, sol - XU) pairs (T) | RNEA link-force parking (rnea NLDS), which
   // also holds the non-power-of-2 reduction (a different phase of each round)
-  extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
   XD* sXD = reinterpret_cast<XD*>(ls_dyn);
   double* fpark = ls_dyn + 2 * P.T + w * LS_PARK;
   double (*part)[4] = reinterpret_cast<double (*)[4]>(fpark);
-  __shared__ double merit[9];
   int step_nz = 0;  // does this lane stage a nonzero step entry sol - XU?
   {
     // chunks of 6 entries per lane with every load issued before the first use (the plain loop
     // waited out a global-memory round trip per entry: ~9 per wave at N = 32)
     constexpr int SU = 6;
-    for (int e0 = threadIdx.x; e0 < P.T; e0 += 64 * W * SU) {
+    for (int e0 = 64 * w + l; e0 < P.T; e0 += 64 * W * SU) {
       double xv[SU], sv[SU];
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
@@ -438,6 +435,23 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 
     st->qp_iters = iter + 1;
     if (stepsize < P.step_tol || iter + 1 >= P.max_iters) active[b] = 0;
   }
+}
+
+template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
+                                                   const double* xu, double* xu_out, const double* __restrict__ sol,
+                                                   const double* __restrict__ goals, const double* __restrict__ fext,
+                                                   int* __restrict__ active,
+                                                   ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
+                                                   int iter, int mode, const double* __restrict__ lin = nullptr,
+                                                   const double* __restrict__ cost = nullptr) {
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
+  __shared__ double merit[9];
+  linesearch_body<SPEC, ABL, W, FW>(Mg, P, b, W > 1 ? (int)(threadIdx.x >> 6) : 0, threadIdx.x & 63, ls_dyn, merit, xu,
+                                    xu_out, sol, goals, fext, active, stats, alpha_out, iter, mode, lin, cost);
 }
 
 // Merit pieces of a given XU (hooks for SQP_OSQP.eepos_cost / integrator_err).

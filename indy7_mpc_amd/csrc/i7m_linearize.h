@@ -61,37 +61,36 @@ __device__ __forceinline__ void imul(double m, const double* h, const double* I,
   o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
 }
 
+// LDS of one wave's linearisation pass (KPW knots): per-link exchange slots, M, RNEA bias.
+struct LinLds {
+  double xs[KPW][6][XS];
+  double sM[KPW][36];
+  double st0[KPW][6];
+};
+constexpr int LINLDS_DOUBLES = (int)(sizeof(LinLds) / sizeof(double));
+
+// The linearisation of knot k of problem b by the six lanes 6g..6g+5 of one wavefront (lane l,
+// g = l / 6 < KPW); `valid` false: the lanes take part in the wave's exchanges but compute and
+// store nothing of use.  The LDS region S belongs to this wave alone (wave_sync only), so the
+// body runs in k_linearize (KPW knots of consecutive problems per wave) and in k_sqp_fused (the
+// knots of one problem, several waves side by side).
 // FW: the external wrench (fext, (B, 6) per problem) is a WORLD-frame spatial force about the
 // world origin (I7M_WRENCH_WORLD); otherwise it is constant in the joint-6 frame (pinocchio
 // f_ext, I7M_WRENCH_LOCAL).
 template <bool SPEC, bool FW = false>
-__global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
-                                                  const double* __restrict__ xu, const double* __restrict__ goals,
-                                                  const double* __restrict__ fext, const int* __restrict__ active,
-                                                  double* __restrict__ lin, double* __restrict__ cost,
-                                                  double* __restrict__ qpd = nullptr, int* __restrict__ init_active = nullptr,
-                                                  ProblemStats* __restrict__ init_stats = nullptr) {
+__device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, const SolveParams& P, const int b,
+                                               const int k, const bool valid, const int l, LinLds& S,
+                                               const double* __restrict__ xu, const double* __restrict__ goals,
+                                               const double* __restrict__ fext, double* __restrict__ lin,
+                                               double* __restrict__ cost, double* __restrict__ qpd) {
   const DevModel& Md = SPEC ? kIndy7Model : *Mg;
-  const int l = threadIdx.x;
   const int g = l / 6;
   const int j = l - 6 * g;
-  const long kg = (long)blockIdx.x * KPW + g;
-  const int b = (int)(kg / P.N);
-  const int k = (int)(kg - (long)b * P.N);
-  const bool valid = (g < KPW) && (b < P.B) && (!active || active[b]);
-  // first SQP iteration: every problem starts active with zeroed stats (knot 0's lanes)
-  if (init_active && g < KPW && b < P.B && k == 0) {
-    if (j == 0) init_active[b] = 1;
-    double* z = reinterpret_cast<double*>(init_stats + b);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) z[3 * j + r] = 0.0;
-  }
   const bool dyn = valid && (k < P.N - 1);
   const int gg = g < KPW ? g : 0;
-
-  __shared__ double xs[KPW][6][XS];
-  __shared__ double sM[KPW][36];
-  __shared__ double st0[KPW][6];
+  auto& xs = S.xs;
+  auto& sM = S.sM;
+  auto& st0 = S.st0;
 
   const double* X = xu + (long)(valid ? b : 0) * P.T + 18 * (valid ? k : 0);
   double v[6];
@@ -281,7 +280,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) { my[4 + r] = Ib[r]; my[13 + r] = Ibd[r]; my[19 + r] = hV[r]; my[25 + r] = F0[r]; }
   }
-  lds_sync();
+  wave_sync();
 
   // ---- 3. subtree sums for link j
   double cm = 0, ch[3] = {0, 0, 0}, cI[6] = {0, 0, 0, 0, 0, 0}, chd[3] = {0, 0, 0}, cId[6] = {0, 0, 0, 0, 0, 0};
@@ -307,14 +306,14 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) ej[r] = bj[r] - cj[r];
   }
-  lds_sync();  // everyone has read the phase-1 slots
+  wave_sync();  // everyone has read the phase-1 slots
   // publish a_j, e_j, S_j for the M row and the derivative columns
   if (g < KPW) {
 #pragma unroll
     for (int r = 0; r < 6; ++r) { my[r] = aj[r]; my[6 + r] = ej[r]; my[12 + r] = Sj[r]; }
     st0[gg][j] = tau0;
   }
-  lds_sync();
+  wave_sync();
   // M row j: M_jk = a_j . S_k (k <= j)
   if (g < KPW) {
 #pragma unroll
@@ -326,7 +325,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
       }
     }
   }
-  lds_sync();
+  wave_sync();
 
   // ---- 4. a = M^-1 (u - tau0) (every lane), dA_j = sum_{i<=j} S_i a_i, g_j = I_j dA_j
   double L[6][6], acc[6];
@@ -353,7 +352,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
 #pragma unroll
     for (int r = 0; r < 6; ++r) my[18 + r] = gI[r];
   }
-  lds_sync();
+  wave_sync();
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (i >= j) {
@@ -445,7 +444,7 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
         my[24 + r] = aq * qj + av * v[j] + bu * uj;
       }
     }
-    lds_sync();
+    wave_sync();
     if (dyn) {
       double sacc = 0.0;
 #pragma unroll
@@ -464,6 +463,32 @@ __global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ M
       }
     }
   }
+}
+
+// KPW consecutive knots of the flattened (problem, knot) index per 64-lane wave.
+template <bool SPEC, bool FW = false>
+__global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
+                                                  const double* __restrict__ xu, const double* __restrict__ goals,
+                                                  const double* __restrict__ fext, const int* __restrict__ active,
+                                                  double* __restrict__ lin, double* __restrict__ cost,
+                                                  double* __restrict__ qpd = nullptr, int* __restrict__ init_active = nullptr,
+                                                  ProblemStats* __restrict__ init_stats = nullptr) {
+  const int l = threadIdx.x;
+  const int g = l / 6;
+  const int j = l - 6 * g;
+  const long kg = (long)blockIdx.x * KPW + g;
+  const int b = (int)(kg / P.N);
+  const int k = (int)(kg - (long)b * P.N);
+  const bool valid = (g < KPW) && (b < P.B) && (!active || active[b]);
+  // first SQP iteration: every problem starts active with zeroed stats (knot 0's lanes)
+  if (init_active && g < KPW && b < P.B && k == 0) {
+    if (j == 0) init_active[b] = 1;
+    double* z = reinterpret_cast<double*>(init_stats + b);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) z[3 * j + r] = 0.0;
+  }
+  __shared__ LinLds S;
+  linearize_body<SPEC, FW>(Mg, P, b, k, valid, l, S, xu, goals, fext, lin, cost, qpd);
 }
 
 }  // namespace i7m

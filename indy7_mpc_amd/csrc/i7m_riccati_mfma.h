@@ -212,7 +212,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
     }
   }
-  lds_sync();
+  wave_sync();
   d4 V;
 #pragma unroll
   for (int i = 0; i < 4; ++i) V[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
@@ -224,13 +224,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     return (long long)__builtin_amdgcn_s_memtime();
   };
   for (int k = N - 2; k >= 0; --k) {
-    lds_sync();
+    wave_sync();
     if (ABL & 512) tm0 = tstamp(V[0]);
     if (ABL & 512) tp = tstamp(p0 + p1 + p2);
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
     if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
-    lds_sync();
+    wave_sync();
     if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
     double bA[4], bB[2];
 #pragma unroll
@@ -297,7 +297,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
             row[2 * lr] = (p >> 2) ? eh1 : eh0;
             row[2 * lr + 1] = (p >> 2) ? eg1 : eg0;
           }
-          lds_sync();
+          wave_sync();
           const double mr0 = col[2 * lq], mr1 = col[2 * lq + 1];
           const double mph = row[2 * lr], mpg = row[2 * lr + 1];
           const double inv = rcp_nr(row[2 * p]);
@@ -331,7 +331,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
           if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
         }
       }
-      lds_sync();
+      wave_sync();
       double E[6];
       const int ncol = HINV ? 25 : 19;
       const int cc = l < ncol ? l : ncol - 1;
@@ -359,7 +359,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
         for (int i = 0; i < 6; ++i) hk[6 * i + (l - 19)] = E[i];
       }
-      lds_sync();
+      wave_sync();
       if (ABL & 512) tm3 = tstamp(E[0]);
       V = mfma(sh[oK[0]], Z10[0], Z00);
       V = mfma(sh[oK[1]], Z10[1], V);
@@ -391,7 +391,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   // reads its block with the same ds_read_b128 sequence (no divergent gathers).
   if (ABL & 1) return;
   constexpr int FB = 20;  // doubles per lane block
-  __syncthreads();  // kbuf stores of the backward sweep -> loads below (same workgroup)
+  wave_sync_all();  // kbuf stores of the backward sweep -> loads below (other lanes of this wave)
   double* S = sol + (long)b * P.T;
   // stage element e of stage k lives at base + k * stride (resolved once per lane)
   auto fbase = [&](int e, int& stride) -> const double* {
@@ -441,12 +441,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       for (int j = 0; j < 19; ++j) r[j] = fk[j % 3] * (j + 1);
       fload(fk, (k + FD < N - 1) ? k + FD : k);
     } else {
-    lds_sync();
+    wave_sync();
     sh[w0] = fk[0];
     sh[w1] = fk[1];
     sh[w2] = fk[2];
     fload(fk, (k + FD < N - 1) ? k + FD : k);
-    lds_sync();
+    wave_sync();
 #pragma unroll
     for (int j = 0; j < 19; ++j) r[j] = myb[j];
     }
@@ -520,13 +520,13 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   const int cc = (l < 12) ? l : 0;
   const int oa = (l < 6) ? DA : DV;  // g_x of lane c < 6 uses Aq' , of lane 6 + j Av'
   for (int k = N - 2; k >= 0; --k) {
-    lds_sync();
+    wave_sync();
     sh[l] = q0;
     sh[l + 64] = q1;
     sh[l + 128] = q2;
     if (l + 192 < DP) sh[l + 192] = q3;
     if (l < 12) sh[DP + l] = preg;
-    lds_sync();
+    wave_sync();
     if (k > 0) { q0 = *src(k - 1, l); q1 = *src(k - 1, l + 64); q2 = *src(k - 1, l + 128); q3 = *src(k - 1, e3); }
     // g_x (lanes 0..11): dq + [p_q + Aq' p_v ; dt p_q + Av' p_v];  g_u (lanes 0..5): dr + Bu' p_v
     double gx = sh[DD + cc] + ((l < 6) ? preg : dt * sh[DP + c6]);
@@ -538,7 +538,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
       gu += sh[DB + 6 * i + c6] * pv;
     }
     if (l < 6) sh[DG + l] = gu;
-    lds_sync();
+    wave_sync();
     double g[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m) g[m] = sh[DG + m];
@@ -552,7 +552,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   }
   // forward: as the main rollout (stage slot K~ 78 | c_v 6 | Aq Av Bu 108), c = 0, x_0 = 0, and
   // the result added to y by the lanes that wrote y's entries
-  __syncthreads();  // kff stores -> loads below
+  wave_sync_all();  // kff stores -> loads below
   double* Y = y + (long)b * P.T;
   const int iv = (l >= 6 && l < 12) ? l - 6 : 0;
   const int ik = l < 6 ? l : 0;
@@ -570,12 +570,12 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   fload(fb, N - 1 > 1 ? 1 : 0);
   double xreg = 0.0;
   auto stage = [&](const int k, double* f) {
-    lds_sync();
+    wave_sync();
     sh[l] = f[0];
     sh[l + 64] = f[1];
     sh[l + 128] = f[2];
     fload(f, (k + 2 < N - 1) ? k + 2 : k);
-    lds_sync();
+    wave_sync();
     double r[19];
     if (l < 6) {
 #pragma unroll

@@ -173,3 +173,61 @@ def test_zero_step_accepts_alpha_one(lib, model):
     h = lib.Handle(model, N=N, max_batch=B)
     al = h.linesearch(XU, XU, goals)
     np.testing.assert_array_equal(al, np.ones(B))
+
+
+@pytest.mark.parametrize("N,B", [(32, 5), (32, 300), (20, 7), (64, 3), (2, 4)])
+def test_fused_pipelines_equal_split(lib, model, N, B):
+    """k_sqp_fused (one launch per solve, and one per SQP iteration) runs the same bodies as the
+    three-kernel path, so its solves are bit-identical to it; B <= 256 takes the 4-wave
+    workgroups, B = 300 the 1-wave ones; a few problems also against the oracle."""
+    xcur, goals, XU = synthetic_batch(B, N, seed=400 + N + B)
+    outs = {}
+    for pipe in (lib.PIPE_SPLIT, lib.PIPE_FUSED, lib.PIPE_FUSED_ITER):
+        h = lib.Handle(model, N=N, max_batch=B, pipeline=pipe)
+        outs[pipe] = h.solve(xcur, goals, XU)
+        h.close()
+    for pipe in (lib.PIPE_FUSED, lib.PIPE_FUSED_ITER):
+        np.testing.assert_array_equal(outs[pipe][0], outs[lib.PIPE_SPLIT][0])
+        for key in ("qp_iters", "n_alphas", "alphas", "n_steps", "stepsizes"):
+            np.testing.assert_array_equal(outs[pipe][1][key], outs[lib.PIPE_SPLIT][1][key])
+    idx = [0, B - 1]
+    _check_sqp(outs[lib.PIPE_FUSED][0][idx], outs[lib.PIPE_FUSED][1][idx], xcur[idx], goals[idx], XU[idx], N=N)
+
+
+@pytest.mark.parametrize("frame", ["local", "world"])
+def test_fused_pipeline_with_wrench(lib, model, frame):
+    N, B = 16, 6
+    xcur, goals, XU = synthetic_batch(B, N, seed=41)
+    f = np.random.default_rng(4).normal(0, 20, (B, 6))
+    outs = []
+    for pipe in (lib.PIPE_SPLIT, lib.PIPE_FUSED):
+        h = lib.Handle(model, N=N, max_batch=B, pipeline=pipe)
+        h.set_external_wrench(f, frame)
+        outs.append(h.solve(xcur, goals, XU))
+        h.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1]["alphas"], outs[1][1]["alphas"])
+
+
+def test_fused_device_solve_out_of_place(lib, model):
+    """The fused path on device buffers: input only read, every output row written (a poisoned
+    problem comes back unchanged), repeated calls give the same answer."""
+    import torch
+
+    N, B = 32, 37
+    xcur, goals, XU = synthetic_batch(B, N, seed=77)
+    goals[5] = np.nan
+    ref, st_ref = lib.Handle(model, N=N, max_batch=B, pipeline=lib.PIPE_SPLIT).solve(xcur, goals, XU)
+    h = lib.Handle(model, N=N, max_batch=B, pipeline=lib.PIPE_FUSED)
+    dev = torch.device("cuda", 0)
+    t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
+    t_out = torch.full_like(t_xu, float("nan"))
+    t_st = torch.zeros(B * lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    h.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(2):
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
+        torch.cuda.synchronize(dev)
+        np.testing.assert_array_equal(t_out.cpu().numpy(), ref)
+        np.testing.assert_array_equal(t_xu.cpu().numpy(), XU)
+        st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=lib.STATS_DTYPE)
+        np.testing.assert_array_equal(st["alphas"], st_ref["alphas"])
