@@ -29,6 +29,8 @@
  *   i7m_aba_derivatives        pin.computeABADerivatives      src/osqp_solver.py:71,76
  *   i7m_rk4                    utils.rk4 (plant)              src/utils.py:3-18
  *   i7m_set_external_wrench    batch_sqp.set_external_wrench_batch  gato_controller.py:129
+ *   i7m_mpc_run                MPC_OSQP.run_mpc over B instances     src/osqp_mpc.py:14-72
+ *                              (batch axis of src/gato_mpc_batch.py:76-217)
  *
  * Layouts (all fp64, C-contiguous, row = problem):
  *   XU    (B, T)  T = 18N-6, [x_0,u_0,x_1,u_1,...,x_{N-1}], x=[q(6),v(6)]  src/osqp_solver.py:22
@@ -190,6 +192,18 @@ int i7m_aba_derivatives(i7m_handle* h, int32_t Bq, const double* q, const double
                         double* dq /*(Bq,6,6)*/, double* dv, double* Minv, double* a);
 int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const double* u, double dt,
             const double* fext, int32_t frame, double* q_out, double* v_out);
+
+/* Closed-loop MPC of B independent instances on the device: MPC_OSQP.run_mpc
+ * (src/osqp_mpc.py:14-72) per instance — goal = endpoints[0] tiled, XU = 0, an initial solve,
+ * then per step: goal distance of xcur (cyclic switch below 0.1, the instance stops above 1.1),
+ * xu_new = SQP solve, the rk4 plant over 0.01 s with the PREVIOUS trajectory's controls, the
+ * warm-start shift and the first / last state pins — all batched, state resident in HBM; the
+ * batch-axis analogue of src/gato_mpc_batch.py:76-217.  xstart (B, 12), endpoints (E, 3);
+ * dist_out (num_steps, B) goal distances (NaN once an instance has stopped); q_out
+ * (num_steps, B, 6) q after each step's plant, xcur_out (B, 12), xu_out (B, T) the final state
+ * and warm start: each may be NULL but dist_out.  Synchronous. */
+int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* endpoints, int32_t n_endpoints,
+                int32_t num_steps, double* dist_out, double* q_out, double* xcur_out, double* xu_out);
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,

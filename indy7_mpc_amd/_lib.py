@@ -123,6 +123,7 @@ SIGNATURES = [
     ("i7m_aba", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_aba_derivatives", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, _DP, _DP, _DP]),
     ("i7m_rk4", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_double, _DP, C.c_int32, _DP, _DP]),
+    ("i7m_mpc_run", C.c_int, [_H, C.c_int32, _DP, _DP, C.c_int32, C.c_int32, _DP, _DP, _DP, _DP]),
     ("i7m_set_timing", C.c_int, [_H, C.c_int]),
     ("i7m_get_kernel_times", C.c_int, [_H, _DP, C.POINTER(C.c_int32), C.c_int32]),
     ("i7m_reset_kernel_times", C.c_int, [_H]),
@@ -331,6 +332,20 @@ class Handle:
         _check(self._lib.i7m_rk4(self._h, n, _ptr(q), _ptr(v), _ptr(u), float(dt), _ptr(f) if f is not None else None,
                                  _FRAMES[frame], _ptr(qo), _ptr(vo)))
         return qo, vo
+
+    def mpc_run(self, xstart, endpoints, num_steps):
+        """Closed-loop MPC of B instances on the device (i7m_mpc_run): returns (dists
+        (num_steps, B), q (num_steps, B, 6), xcur (B, 12), XU (B, T))."""
+        xs = _f64(xstart).reshape(-1, NX)
+        ep = _f64(endpoints).reshape(-1, 3)
+        B = xs.shape[0]
+        d = np.empty((num_steps, B))
+        q = np.empty((num_steps, B, NJ))
+        xc = np.empty((B, NX))
+        xu = np.empty((B, self.T))
+        _check(self._lib.i7m_mpc_run(self._h, B, _ptr(xs), _ptr(ep), ep.shape[0], int(num_steps), _ptr(d), _ptr(q),
+                                     _ptr(xc), _ptr(xu)))
+        return d, q, xc, xu
 
     # ---- timing --------------------------------------------------------------------------
     def set_stream(self, stream_ptr: int):

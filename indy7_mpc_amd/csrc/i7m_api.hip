@@ -20,6 +20,7 @@
 #include "i7m_linearize.h"
 #include "i7m_riccati_mfma.h"
 #include "i7m_box.h"
+#include "i7m_mpc.h"
 
 // Source hash of the tree this library was built from (__graft_entry__.build passes it), so
 // tests and smoke() can check that the loaded binary matches the sources they run against.
@@ -909,6 +910,71 @@ int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
     HIPCHK(hipStreamSynchronize(h->stream));
   }
   return I7M_OK;
+}
+
+int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* endpoints, int32_t n_endpoints,
+                int32_t num_steps, double* dist_out, double* q_out, double* xcur_out, double* xu_out) {
+  int rc = check_batch(h, B, 3);
+  if (rc) return rc;
+  if (n_endpoints < 1 || num_steps < 0 || !endpoints || !xstart || !dist_out)
+    return fail(I7M_EINVAL, "mpc_run: need xstart, >= 1 endpoint, num_steps >= 0, dist_out");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const int N = h->cfg.N;
+  const size_t T = 18 * (size_t)N - 6;
+  // per-run state beyond the handle's buffers (this is a whole closed-loop run, not the solve
+  // hot path): endpoints, goal index, alive flag, the distance and q histories
+  double *d_ep = nullptr, *d_dist = nullptr, *d_q = nullptr;
+  int *d_gi = nullptr, *d_alive = nullptr;
+  auto cleanup = [&]() {
+    for (void* p : {(void*)d_ep, (void*)d_dist, (void*)d_q, (void*)d_gi, (void*)d_alive})
+      if (p) (void)hipFree(p);
+  };
+  const size_t hist = (size_t)std::max(num_steps, 1) * B;
+  if (hipMalloc(&d_ep, 3 * 8 * (size_t)n_endpoints) != hipSuccess || hipMalloc(&d_dist, 8 * hist) != hipSuccess ||
+      hipMalloc(&d_q, 6 * 8 * hist) != hipSuccess || hipMalloc(&d_gi, 4 * (size_t)B) != hipSuccess ||
+      hipMalloc(&d_alive, 4 * (size_t)B) != hipSuccess) {
+    cleanup();
+    return fail(I7M_ENOMEM, "mpc_run: device allocation failed");
+  }
+  auto run = [&]() -> int {
+    // src/osqp_mpc.py:14-27: goal = endpoint 0 tiled, XU = 0, XU = sqp(xcur, goal, XU)
+    std::vector<double> goals((size_t)B * 3 * N);
+    for (size_t b = 0; b < (size_t)B; ++b)
+      for (int k = 0; k < N; ++k)
+        for (int r = 0; r < 3; ++r) goals[(b * N + k) * 3 + r] = endpoints[r];
+    std::vector<int> ones((size_t)B, 1);
+    int rc2;
+    if ((rc2 = copy_in(h, h->d_xs, xstart, (size_t)B * 12))) return rc2;
+    if ((rc2 = copy_in(h, h->d_goal, goals.data(), goals.size()))) return rc2;
+    if ((rc2 = copy_in(h, d_ep, endpoints, 3 * (size_t)n_endpoints))) return rc2;
+    HIPCHK(hipMemsetAsync(d_gi, 0, 4 * (size_t)B, h->stream));
+    HIPCHK(hipMemcpyAsync(d_alive, ones.data(), 4 * (size_t)B, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->d_xu, 0, 8 * (size_t)B * T, h->stream));
+    if ((rc2 = run_sqp(h, B, h->d_xu, h->d_xu, h->d_xs, h->d_goal, 3, h->d_stats))) return rc2;
+    for (int i = 0; i < num_steps; ++i) {
+      hipLaunchKernelGGL(k_mpc_goal, dim3((B + 255) / 256), dim3(256), 0, h->stream, h->d_model, B, N, h->d_xs, h->d_goal,
+                         d_ep, n_endpoints, d_gi, d_alive, d_dist + (size_t)i * B);
+      HIPCHK(hipGetLastError());
+      // xu_new = sqp(xcur, goal, XU) into the scratch buffer d_out (XU itself is read only)
+      if ((rc2 = run_sqp(h, B, h->d_xu, h->d_out, h->d_xs, h->d_goal, 3, h->d_stats))) return rc2;
+      hipLaunchKernelGGL(k_mpc_advance, dim3(B), dim3(64), 0, h->stream, h->d_model, B, N, h->cfg.dt, h->d_xs, h->d_xu,
+                         h->d_out, d_alive, d_q + (size_t)i * B * 6);
+      HIPCHK(hipGetLastError());
+    }
+    if (num_steps > 0) {
+      if ((rc2 = copy_out(h, dist_out, d_dist, (size_t)num_steps * B))) return rc2;
+      if (q_out && (rc2 = copy_out(h, q_out, d_q, (size_t)num_steps * B * 6))) return rc2;
+    }
+    if (xcur_out && (rc2 = copy_out(h, xcur_out, h->d_xs, (size_t)B * 12))) return rc2;
+    if (xu_out && (rc2 = copy_out(h, xu_out, h->d_xu, (size_t)B * T))) return rc2;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return I7M_OK;
+  };
+  rc = run();
+  (void)hipStreamSynchronize(h->stream);
+  cleanup();
+  return rc;
 }
 
 int i7m_set_timing(i7m_handle* h, int enable) {

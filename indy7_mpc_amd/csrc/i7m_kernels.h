@@ -549,36 +549,42 @@ __global__ void __launch_bounds__(256) k_abad(const DevModel* __restrict__ Mg, i
 // fext_world: fext is a world-frame wrench, converted to joint 6's frame ONCE at the start
 // configuration q and held for the four stages, as the reference's host plant does
 // (src/gato_mpc_batch_sample.py:270-279: actInv at x_last, then rk4 with that local force).
+// One plant step of one lane: q, v, u (6 each) -> qo, vo; f6 a local joint-6 wrench or null.
+__device__ __forceinline__ void rk4_step(const DevModel& Md, const double* q, const double* v, const double* u, double dt,
+                                         const double* f6, bool fext_world, double* qo, double* vo) {
+  double q0[6], v0[6], uu[6], c[6], s[6], L[6][6], fl[6];
+  for (int r = 0; r < 6; ++r) { q0[r] = q[r]; v0[r] = v[r]; uu[r] = u[r]; }
+  double k1v[6], k2v[6], k3v[6], k4v[6], k2q[6], k3q[6], k4q[6], qq[6];
+  sincos6(q0, c, s);
+  if (f6 && fext_world) {
+    wrench_world_to_local(Md, c, s, f6, fl);
+    f6 = fl;
+  }
+  forward_dynamics(Md, c, s, v0, uu, f6, L, k1v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + v0[r] * dt / 2; k2q[r] = v0[r] + k1v[r] * dt / 2; }
+  sincos6(qq, c, s);
+  forward_dynamics(Md, c, s, k2q, uu, f6, L, k2v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k2q[r] * dt / 2; k3q[r] = v0[r] + k2v[r] * dt / 2; }
+  sincos6(qq, c, s);
+  forward_dynamics(Md, c, s, k3q, uu, f6, L, k3v);
+  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k3q[r] * dt; k4q[r] = v0[r] + k3v[r] * dt; }
+  sincos6(qq, c, s);
+  forward_dynamics(Md, c, s, k4q, uu, f6, L, k4v);
+  for (int r = 0; r < 6; ++r) {
+    vo[r] = v0[r] + (dt / 6) * (k1v[r] + 2 * k2v[r] + 2 * k3v[r] + k4v[r]);
+    const double avg = (v0[r] + 2 * k2q[r] + 2 * k3q[r] + k4q[r]) / 6;
+    qo[r] = q0[r] + avg * dt;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_rk4(const DevModel* __restrict__ Mg, int n, const double* __restrict__ q,
                                              const double* __restrict__ v, const double* __restrict__ u, double dt,
                                              const double* __restrict__ fext, int fext_world, double* __restrict__ qo,
                                              double* __restrict__ vo) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double* f6 = fext ? fext + 6L * i : nullptr;
-  double q0[6], v0[6], uu[6], c[6], s[6], L[6][6], fl[6];
-  for (int r = 0; r < 6; ++r) { q0[r] = q[6L * i + r]; v0[r] = v[6L * i + r]; uu[r] = u[6L * i + r]; }
-  double k1v[6], k2v[6], k3v[6], k4v[6], k2q[6], k3q[6], k4q[6], qq[6];
-  sincos6(q0, c, s);
-  if (f6 && fext_world) {
-    wrench_world_to_local(*Mg, c, s, f6, fl);
-    f6 = fl;
-  }
-  forward_dynamics(*Mg, c, s, v0, uu, f6, L, k1v);
-  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + v0[r] * dt / 2; k2q[r] = v0[r] + k1v[r] * dt / 2; }
-  sincos6(qq, c, s);
-  forward_dynamics(*Mg, c, s, k2q, uu, f6, L, k2v);
-  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k2q[r] * dt / 2; k3q[r] = v0[r] + k2v[r] * dt / 2; }
-  sincos6(qq, c, s);
-  forward_dynamics(*Mg, c, s, k3q, uu, f6, L, k3v);
-  for (int r = 0; r < 6; ++r) { qq[r] = q0[r] + k3q[r] * dt; k4q[r] = v0[r] + k3v[r] * dt; }
-  sincos6(qq, c, s);
-  forward_dynamics(*Mg, c, s, k4q, uu, f6, L, k4v);
-  for (int r = 0; r < 6; ++r) {
-    vo[6L * i + r] = v0[r] + (dt / 6) * (k1v[r] + 2 * k2v[r] + 2 * k3v[r] + k4v[r]);
-    const double avg = (v0[r] + 2 * k2q[r] + 2 * k3q[r] + k4q[r]) / 6;
-    qo[6L * i + r] = q0[r] + avg * dt;
-  }
+  rk4_step(*Mg, q + 6L * i, v + 6L * i, u + 6L * i, dt, fext ? fext + 6L * i : nullptr, fext_world != 0, qo + 6L * i,
+           vo + 6L * i);
 }
 
 }  // namespace i7m

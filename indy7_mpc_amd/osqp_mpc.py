@@ -65,3 +65,16 @@ class MPC_OSQP:
             XU[:nx] = xcur.reshape(-1)
             XU[-nx:] = np.hstack([np.ones(nq), np.zeros(nv)])
         return self.xpath
+
+    def run_mpc_batch(self, xstart_batch, endpoints, num_steps=500):
+        """``run_mpc`` for B independent instances at once, every step on the GPU (i7m_mpc_run:
+        goal switching, the batched SQP, the rk4 plant and the warm-start shift and pins of
+        :14-72 per instance; the batch axis of src/gato_mpc_batch.py:76-217).  Returns
+        (q_path (num_steps, B, 6), goal_distances (num_steps, B)); an instance that stops (goal
+        distance > 1.1) has NaN from the step after its last distance on."""
+        xs = np.asarray(xstart_batch, dtype=float).reshape(-1, self.solver.nx)
+        h = self.sqp_optimizer._handle_for(xs.shape[0])
+        d, q, xc, xu = h.mpc_run(xs, np.asarray(endpoints, dtype=float).reshape(-1, 3), num_steps)
+        self.batch_xcur, self.batch_XU = xc, xu
+        return q, d
+

@@ -1,0 +1,78 @@
+"""GPU: the batched closed-loop MPC driver (i7m_mpc_run / MPC_OSQP.run_mpc_batch): B independent
+instances of the reference's MPC_OSQP.run_mpc (src/osqp_mpc.py:14-72) stepped together on the
+device, each against its own oracle run (oracle/mpc_ref.py).
+
+Tolerance: 2e-6 absolute on goal distances and q over 8 steps (both sides solve every QP
+exactly; only rounding differs, amplified by the closed loop).  Instance 0 is the notebook's
+run (notebooks/pin_mpc_indy7.ipynb cell 2), so its first distances also meet the reference's
+printed trace.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rbd
+from oracle.mpc_ref import run_mpc_ref
+from oracle.osqp_ref import OSQPSolverRef, SQPRef
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from indy7_mpc_amd import _lib
+    _lib.load()
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible but the gpu tests were requested")
+    return _lib
+
+
+def test_batched_closed_loop_matches_independent_oracle_runs(lib, model):
+    from indy7_mpc_amd.osqp_mpc import MPC_OSQP
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    ends = np.array([rbd.eepos(np.array(q)) for q in tr["endpoint_q"]])
+    steps = 8
+    rng = np.random.default_rng(8)
+    xs = np.zeros((5, 12))
+    xs[0] = tr["xstart"]                                            # the notebook's run
+    xs[1, :6] = np.array(tr["endpoint_q"][0]) + 0.01                # starts within 0.1 of goal 0: switches
+    xs[2, :6], xs[2, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
+    xs[3, :6] = [0.4, -1.9, -0.6, -2.0, -0.1, 0.4]                  # 1.86 from the goal: stops at once
+    xs[4, :6], xs[4, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
+    solver = OSQPSolver(model)
+    ctrl = MPC_OSQP(model, SQP_OSQP(solver), solver)
+    q, d = ctrl.run_mpc_batch(xs, ends, num_steps=steps)
+    assert q.shape == (steps, 5, 6) and d.shape == (steps, 5)
+    for b in range(5):
+        xpath, dists = run_mpc_ref(SQPRef(OSQPSolverRef(N=32)), xs[b], ends, num_steps=steps)
+        n = len(dists)
+        np.testing.assert_allclose(d[:n, b], dists, rtol=0, atol=2e-6)
+        assert np.isnan(d[n:, b]).all()
+        n_plant = len(xpath)  # the stopping step records a distance but no plant step
+        np.testing.assert_allclose(q[:n_plant, b], np.array(xpath).reshape(n_plant, 6), rtol=0, atol=2e-6)
+        assert np.isnan(q[n_plant:, b]).all()
+    assert np.isnan(d[1:, 3]).all() and d[0, 3] > 1.1
+    ref = np.array(tr["goal_distances"][:steps])
+    assert abs(d[0, 0] - ref[0]) < 1e-15 and np.abs(d[:, 0] - ref).max() < 2e-6
+
+
+def test_batched_closed_loop_instances_are_independent(lib, model):
+    """Identical instances evolve identically (src/gato_mpc_batch.py:124-134's consistency check)
+    and an instance's trajectory does not depend on its batch neighbours."""
+    h = lib.Handle(model, N=32, max_batch=16)
+    ends = np.array([rbd.eepos(np.full(6, 0.3)), rbd.eepos(np.full(6, 0.9))])
+    xs = np.tile(np.ones(12), (16, 1))
+    xs[8:, :6] = 0.5
+    d, q, xc, xu = h.mpc_run(xs, ends, 5)
+    for b in range(8):
+        np.testing.assert_array_equal(q[:, b], q[:, 0])
+        np.testing.assert_array_equal(q[:, 8 + b], q[:, 8])
+    d1, q1, _, _ = h.mpc_run(xs[8:9], ends, 5)
+    np.testing.assert_array_equal(q1[:, 0], q[:, 8])
+    np.testing.assert_array_equal(xc[:, :6], q[-1])
