@@ -234,6 +234,29 @@ def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: 
             "finite": bool(np.isfinite(out).all())}
 
 
+def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps: int = 20):
+    """The batched closed loop (MPC_OSQP.run_mpc for B instances, i7m_mpc_run: goal update, SQP,
+    rk4 plant, shift and pins per MPC step, all on the device; src/osqp_mpc.py:14-72 and the batch
+    axis of src/gato_mpc_batch.py:76-217): instance-steps per second over `steps` MPC steps of the
+    config-3 draws, one synchronous call (with its H2D of the start states and D2H of the
+    histories), after one warm-up call."""
+    from indy7_mpc_amd import _lib
+    from indy7_mpc_amd.synthetic import draw_states
+
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local)
+    h.set_stream(stream.cuda_stream)
+    xs, qg = draw_states(model, B, seed=42 + 3)
+    ends = np.vstack([h.eepos(qg[:1]), h.eepos(qg[1:2])])
+    h.mpc_run(xs, ends, 2)
+    t0 = time.perf_counter()
+    d, q, _, _ = h.mpc_run(xs, ends, steps)
+    el = time.perf_counter() - t0
+    h.close()
+    return {"workload": f"closed-loop MPC: B={B} instances, N={N}, {steps} MPC steps (SQP + rk4 plant + shift)",
+            "value": B * steps / el, "unit": "instance-steps/s", "ms_per_mpc_step": 1e3 * el / steps,
+            "instances_alive_at_end": int(np.isfinite(d[-1]).sum()), "finite": bool(np.isfinite(q[np.isfinite(q)]).all())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -388,6 +411,7 @@ def main():
     cpu = None if native is None else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads, native)
     c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1)
     c2 = None if (args.no_config2 or world > 1) else config2(model, stream, local, 200, 10)
+    mpc = None if (args.no_config2 or world > 1) else mpc_closed_loop(model, stream, local, B, N)
     out = {
         "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
         "value": value,
@@ -457,6 +481,8 @@ def main():
         out["config2"] = c2
     if c4 is not None:
         out["config4"] = c4
+    if mpc is not None:
+        out["mpc_closed_loop"] = mpc
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -1,12 +1,12 @@
 #!/bin/bash
 # One GPU-box session: tests, bench, rocprof kernel trace + PMC passes of the headline (config 3)
 # and of config 4.  Every GPU step has its own time limit; the chain stops at the first failure.
-#   TAG=r02 [STEPS=tests,bench,trace,pmc,c4] bash tools/gpu_round.sh
+#   TAG=r02 [STEPS=tests,bench,trace,pmc,c4,fused] bash tools/gpu_round.sh
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${TAG:-run}
-STEPS=${STEPS:-tests,bench,trace,pmc,c4}
+STEPS=${STEPS:-tests,bench,trace,pmc,c4,fused}
 mkdir -p $O
 cd $R
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
@@ -36,5 +36,12 @@ if has c4; then
   python $R/tools/trace_summary.py $O/c4_trace/run_kernel_trace.csv --batch 4096 --N 64 > $O/c4_trace_summary.json
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c4_fetch -o fetch -- python $R/tools/profile_kernels.py --box --N 64 --steps 1 --warmup 1 > $O/c4_fetch.log 2>&1 || { tail -20 $O/c4_fetch.log; exit 8; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/c4_write -o write -- python $R/tools/profile_kernels.py --box --N 64 --steps 1 --warmup 1 > $O/c4_write.log 2>&1 || { tail -20 $O/c4_write.log; exit 9; }
+fi
+if has fused; then
+  # the fused pipeline (k_sqp_fused, one launch per solve) at the bench shape: trace + FETCH / WRITE
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/fused_trace -o run -- python $R/tools/profile_kernels.py --pipeline fused --steps 4 > $O/fused_trace.log 2>&1 || { tail -20 $O/fused_trace.log; exit 10; }
+  python $R/tools/trace_summary.py $O/fused_trace/run_kernel_trace.csv --batch 4096 > $O/fused_trace_summary.json
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fused_fetch -o fetch -- python $R/tools/profile_kernels.py --pipeline fused --steps 2 > $O/fused_fetch.log 2>&1 || { tail -20 $O/fused_fetch.log; exit 11; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/fused_write -o write -- python $R/tools/profile_kernels.py --pipeline fused --steps 2 > $O/fused_write.log 2>&1 || { tail -20 $O/fused_write.log; exit 12; }
 fi
 ls -R $O | head -60

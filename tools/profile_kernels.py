@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--box", action="store_true", help="config 4: box rows (I7M_QP_BOX), seed 46")
+    ap.add_argument("--pipeline", default="split", choices=["split", "fused", "fused_iter"])
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -27,7 +28,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     model = default_model()
-    h = _lib.Handle(model, N=a.N, max_batch=a.batch, **({"qp_mode": _lib.QP_BOX} if a.box else {}))
+    pipe = {"split": _lib.PIPE_SPLIT, "fused": _lib.PIPE_FUSED, "fused_iter": _lib.PIPE_FUSED_ITER}[a.pipeline]
+    h = _lib.Handle(model, N=a.N, max_batch=a.batch, pipeline=pipe, **({"qp_mode": _lib.QP_BOX} if a.box else {}))
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
     h.set_stream(s.cuda_stream)
