@@ -76,3 +76,25 @@ def test_batched_closed_loop_instances_are_independent(lib, model):
     d1, q1, _, _ = h.mpc_run(xs[8:9], ends, 5)
     np.testing.assert_array_equal(q1[:, 0], q[:, 8])
     np.testing.assert_array_equal(xc[:, :6], q[-1])
+
+
+def test_notebook_500_step_trace_qualitative(lib, model):
+    """The notebook's whole closed-loop run (pin_mpc_indy7.ipynb:98-597, 500 printed goal
+    distances) on the device (i7m_mpc_run, B = 1).  The reference solved each QP with OSQP at
+    eps 1e-3 and this solver solves it exactly, so the chaotic closed loop drifts: the first 8
+    steps match to 2e-6 (test_mpc_osqp_closed_loop_matches_notebook), the rest qualitatively:
+    no goal switch and no break in 500 steps in either, the same peak step, distances within
+    0.05 everywhere (max measured 0.026, steps 100-200) and 0.005 over the last 100 steps, the
+    same settling value to 3 %."""
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    h = lib.Handle(model, N=32, max_batch=1)
+    ends = h.eepos(np.array(tr["endpoint_q"]))
+    d, q, xc, xu = h.mpc_run(np.array([tr["xstart"]]), ends, 500)
+    d = d[:, 0]
+    ref = np.array(tr["goal_distances"])
+    assert np.isfinite(d).all()                       # no break (> 1.1)
+    assert (d >= 0.1).all() and (ref >= 0.1).all()    # no goal switch (< 0.1)
+    assert int(np.argmax(d)) == int(np.argmax(ref))
+    assert np.abs(d - ref).max() < 0.05
+    assert np.abs(d[-100:] - ref[-100:]).max() < 5e-3
+    assert abs(d[-1] - ref[-1]) < 0.03 * ref[-1]
