@@ -29,7 +29,26 @@
 namespace i7m {
 
 constexpr int KPW = 10;   // knots per wavefront
-constexpr int XS = 32;    // LDS doubles per link slot
+constexpr int XS = 20;    // LDS doubles per link slot (round 1 uses 19)
+
+// Where the 6x6 factor of M lives: 0 = every lane's registers (chol6; default), 1 = LDS,
+// factorised by the knot's six lanes together (21 doubles fewer per lane).  Measured on
+// MI355X at B = 4096: registers 96.1 us, LDS 99.7 us per launch.
+#ifndef I7M_LIN_CHOL_LDS
+#define I7M_LIN_CHOL_LDS 0
+#endif
+
+// Occupancy target of k_linearize (amdgpu_waves_per_eu): 0 = the compiler's choice (242 VGPRs,
+// 2 waves per SIMD; default).  3 caps it at 168 VGPRs (its 12.7 KB of LDS allows 3 waves) and
+// spills 21-42 VGPRs: 105-118 us against 96 us.
+#ifndef I7M_LIN_WPE
+#define I7M_LIN_WPE 0
+#endif
+#if I7M_LIN_WPE > 0
+#define I7M_LIN_OCC __attribute__((amdgpu_waves_per_eu(I7M_LIN_WPE, I7M_LIN_WPE)))
+#else
+#define I7M_LIN_OCC
+#endif
 
 // spatial helpers on 6-vectors [lin; ang]
 __device__ __forceinline__ void mcross(const double* a, const double* b, double* o) {  // a x b (motion)
@@ -59,6 +78,25 @@ __device__ __forceinline__ void imul(double m, const double* h, const double* I,
   o[3] = I[0] * x[3] + I[1] * x[4] + I[2] * x[5] + (h[1] * x[2] - h[2] * x[1]);
   o[4] = I[1] * x[3] + I[3] * x[4] + I[4] * x[5] + (h[2] * x[0] - h[0] * x[2]);
   o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
+}
+
+// Solve L L^T x = b in place, L from chol6's layout (strict lower triangle = L, diagonal =
+// 1 / L_jj), row-major 6x6 in LDS, read entry by entry (the operation order of chol6_solve).
+__device__ __forceinline__ void chol6_solve_lds(const double* Lm, double b[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double v = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) v -= Lm[6 * i + k] * b[k];
+    b[i] = v * Lm[6 * i + i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double v = b[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) v -= Lm[6 * k + i] * b[k];
+    b[i] = v * Lm[6 * i + i];
+  }
 }
 
 // LDS of one wave's linearisation pass (KPW knots): per-link exchange slots, M, RNEA bias.  16-byte
@@ -193,9 +231,14 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
     }
   }
 
-  // ---- 2. own link: world inertia (m, h, Ib), its rate (hd, Ibd), momentum, bias force
+  // ---- 2. own link: world inertia (m, h, Ib), its rate (hd, Ibd), momentum hV, bias force F0.
+  // Everything that needs the link's placement (Rj, pj) is formed here, so it dies after this
+  // block; the publish/sum rounds below keep the subtree sums' live ranges short (DESIGN.md §4.1:
+  // the register peak decides the waves per SIMD).
   const double m = Md.m[j];
-  double h[3], Ib[6], hV[6], F0[6], hd[3], Ibd[6];
+  double h[3], Ib[6], hV[6], F0[6];
+  double* my = &xs[gg][j][0];
+  double cm = 0, ch[3] = {0, 0, 0}, cI[6] = {0, 0, 0, 0, 0, 0}, chd[3] = {0, 0, 0}, cId[6] = {0, 0, 0, 0, 0, 0};
   {
     const double* hl = Md.h[j];
     const double* Io = Md.Io[j];
@@ -252,6 +295,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
     // rate: hd = m v + w x h ; Ibd = [w]x Ib - Ib [w]x - h v^T - v h^T + 2 (v.h) I
     const double* vl = Vj;
     const double* w = Vj + 3;
+    double hd[3], Ibd[6];
     hd[0] = m * vl[0] + (w[1] * h[2] - w[2] * h[1]);
     hd[1] = m * vl[1] + (w[2] * h[0] - w[0] * h[2]);
     hd[2] = m * vl[2] + (w[0] * h[1] - w[1] * h[0]);
@@ -272,21 +316,16 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
       if (r == qq) val += 2.0 * vh;
       Ibd[e] = val;
     }
-  }
-  // publish: [0]m [1..3]h [4..9]Ib [10..12]hd [13..18]Ibd [19..24]hV [25..30]F0
-  double* my = &xs[gg][j][0];
-  if (g < KPW) {
-    my[0] = m;
+    // round 1: [0]m [1..3]h [4..9]Ib [10..12]hd [13..18]Ibd -> the inertia sums IC_j, dIC_j
+    if (g < KPW) {
+      my[0] = m;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) { my[1 + r] = h[r]; my[10 + r] = hd[r]; }
+      for (int r = 0; r < 3; ++r) { my[1 + r] = h[r]; my[10 + r] = hd[r]; }
 #pragma unroll
-    for (int r = 0; r < 6; ++r) { my[4 + r] = Ib[r]; my[13 + r] = Ibd[r]; my[19 + r] = hV[r]; my[25 + r] = F0[r]; }
+      for (int r = 0; r < 6; ++r) { my[4 + r] = Ib[r]; my[13 + r] = Ibd[r]; }
+    }
   }
   wave_sync();
-
-  // ---- 3. subtree sums for link j
-  double cm = 0, ch[3] = {0, 0, 0}, cI[6] = {0, 0, 0, 0, 0, 0}, chd[3] = {0, 0, 0}, cId[6] = {0, 0, 0, 0, 0, 0};
-  double HC[6] = {0, 0, 0, 0, 0, 0}, Fc[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (i >= j) {
@@ -295,21 +334,60 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
 #pragma unroll
       for (int r = 0; r < 3; ++r) { ch[r] += o[1 + r]; chd[r] += o[10 + r]; }
 #pragma unroll
-      for (int r = 0; r < 6; ++r) { cI[r] += o[4 + r]; cId[r] += o[13 + r]; HC[r] += o[19 + r]; Fc[r] += o[25 + r]; }
+      for (int r = 0; r < 6; ++r) { cI[r] += o[4 + r]; cId[r] += o[13 + r]; }
     }
   }
+  wave_sync();  // every lane has read round 1
+  // round 2: [0..5]hV [6..11]F0 -> the momentum and force sums HC_j, F^c_j (without the
+  // M^-1 (u - tau0) acceleration, which follows in step 4)
+  if (g < KPW) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { my[r] = hV[r]; my[6 + r] = F0[r]; }
+  }
+  wave_sync();
+  double HC[6] = {0, 0, 0, 0, 0, 0}, Fc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (i >= j) {
+      const double* o = &xs[gg][i][0];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) { HC[r] += o[r]; Fc[r] += o[6 + r]; }
+    }
+  }
+
+  // ---- 3. everything of link j that does not need the joint accelerations: a_j, e_j, z_j,
+  // W_j, the acceleration-free parts of Z_j and y_j, and from them the acceleration-free part of
+  // column j of dtau/dq and all of column j of dtau/dv.  dIC, HC, F^c, V, A0 die here.
   const double tau0 = dot6(Sj, Fc);
-  double aj[6], ej[6];
+  double aj[6], ej[6], zj[6], Wj[6], Zp[6], yp[6];
   imul(cm, ch, cI, Sj, aj);
   {
-    double bj[6], cj[6];
+    double bj[6], cj[6], t2[6];
     imul(0.0, chd, cId, Sj, bj);
     fcross(Sj, HC, cj);
 #pragma unroll
     for (int r = 0; r < 6; ++r) ej[r] = bj[r] - cj[r];
+    mcross(Sj, Vj, Wj);
+    imul(cm, ch, cI, Wj, t2);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) zj[r] = bj[r] - 2.0 * t2[r] + cj[r];
   }
-  wave_sync();  // everyone has read the phase-1 slots
-  // publish a_j, e_j, S_j for the M row and the derivative columns
+  {
+    double t1[6], t2[6];
+    mcross(Sj, A0j, t1);
+    mcross(Wj, Vj, t2);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) Zp[r] = t1[r] - t2[r];
+    double a1[6], a2[6], a3[6], a4[6];
+    fcross(Sj, Fc, a1);
+    imul(cm, ch, cI, Zp, a2);
+    imul(0.0, chd, cId, Wj, a3);
+    fcross(Wj, HC, a4);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) yp[r] = a1[r] - a2[r] - a3[r] - a4[r];
+  }
+  wave_sync();  // every lane has read round 2
+  // round 3: [0..5]a_j [6..11]e_j [12..17]S_j (kept to the end: M row, dA, derivative rows)
   if (g < KPW) {
 #pragma unroll
     for (int r = 0; r < 6; ++r) { my[r] = aj[r]; my[6 + r] = ej[r]; my[12 + r] = Sj[r]; }
@@ -327,76 +405,16 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
       }
     }
   }
-  wave_sync();
-
-  // ---- 4. a = M^-1 (u - tau0) (every lane), dA_j = sum_{i<=j} S_i a_i, g_j = I_j dA_j
-  double L[6][6], acc[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) L[r][cc] = sM[gg][6 * r + cc];
-  chol6(L);
-#pragma unroll
-  for (int r = 0; r < 6; ++r) acc[r] = (dyn ? X[12 + r] : 0.0) - st0[gg][r];
-  chol6_solve(L, acc);
-  double dA[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    if (i <= j) {
-      const double* Si = &xs[gg][i][12];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) dA[r] += Si[r] * acc[i];
-    }
-  }
-  double gI[6];
-  imul(m, h, Ib, dA, gI);
-  if (g < KPW) {
-#pragma unroll
-    for (int r = 0; r < 6; ++r) my[18 + r] = gI[r];
-  }
-  wave_sync();
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    if (i >= j) {
-#pragma unroll
-      for (int r = 0; r < 6; ++r) Fc[r] += xs[gg][i][18 + r];
-    }
-  }
-  // ---- 5. W, Z, y, z of link j
-  double Wj[6], Zj[6], yj[6], zj[6];
-  {
-    double Aj[6], t1[6], t2[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) Aj[r] = A0j[r] + dA[r];
-    mcross(Sj, Vj, Wj);
-    mcross(Sj, Aj, t1);
-    mcross(Wj, Vj, t2);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) Zj[r] = t1[r] - t2[r];
-    double a1[6], a2[6], a3[6], a4[6];
-    fcross(Sj, Fc, a1);
-    imul(cm, ch, cI, Zj, a2);
-    imul(0.0, chd, cId, Wj, a3);
-    fcross(Wj, HC, a4);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) yj[r] = a1[r] - a2[r] - a3[r] - a4[r];
-    double b1[6], b2[6], b3[6];
-    imul(0.0, chd, cId, Sj, b1);
-    imul(cm, ch, cI, Wj, b2);
-    fcross(Sj, HC, b3);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) zj[r] = b1[r] - 2.0 * b2[r] + b3[r];
-  }
-  // ---- 6. column j of dtau/dq, dtau/dv, then -M^-1 and outputs
+  // column j: dv (complete) and dq without the terms of dA = sum S_i a_i (added in step 4)
   double dq[6], dv[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     const double* o = &xs[gg][r][0];
     if (r >= j) {
-      dq[r] = -(dot6(o, Zj) + dot6(o + 6, Wj));
+      dq[r] = -(dot6(o, Zp) + dot6(o + 6, Wj));
       dv[r] = dot6(o + 6, Sj) - 2.0 * dot6(o, Wj);
     } else {
-      dq[r] = dot6(o + 12, yj);
+      dq[r] = dot6(o + 12, yp);
       dv[r] = dot6(o + 12, zj);
     }
   }
@@ -413,50 +431,163 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
 #pragma unroll
     for (int r = 0; r < 6; ++r) dq[r] += dot6(&xs[gg][r][12], tS);
   }
-  chol6_solve(L, dq);
-  chol6_solve(L, dv);
-  double em[6] = {0, 0, 0, 0, 0, 0};
-  em[j] = 1.0;
-  chol6_solve(L, em);
-  if (dyn) {
-    double* out = lin + ((long)b * (P.N - 1) + k) * LIN_STRIDE;
-    const double dt = P.dt;
+  wave_sync();
+
+#if I7M_LIN_CHOL_LDS
+  // ---- 4. M = L L^T, factorised by the knot's six lanes together (lane r holds row r; column c
+  // is closed by lane c, then by the lanes r > c, the finished rows passing through sM).  Same
+  // operation order as chol6, so the same factor; it overwrites M in sM and stays there for
+  // the solves (chol6_solve_lds): no lane holds the whole factor in registers.
+  {
+    double Lr[6];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      out[6 * r + j] = -dt * dq[r];
-      out[36 + 6 * r + j] = (r == j ? 1.0 : 0.0) - dt * dv[r];
-      if (r <= j) {
-        out[72 + 6 * r + j] = dt * em[r];
-        out[72 + 6 * j + r] = dt * em[r];
+    for (int cc = 0; cc < 6; ++cc) Lr[cc] = sM[gg][6 * j + cc];
+    wave_sync();  // every lane has read its row of M
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      if (j == c) {
+        double d = Lr[c];
+#pragma unroll
+        for (int kk = 0; kk < c; ++kk) d -= Lr[kk] * Lr[kk];
+        Lr[c] = rsqrt_nr(d);
+        if (g < KPW) {
+#pragma unroll
+          for (int kk = 0; kk <= c; ++kk) sM[gg][6 * c + kk] = Lr[kk];
+        }
+      }
+      wave_sync();
+      if (j > c) {
+        const double* Lc = &sM[gg][6 * c];
+        double v = Lr[c];
+#pragma unroll
+        for (int kk = 0; kk < c; ++kk) v -= Lr[kk] * Lc[kk];
+        Lr[c] = v * Lc[c];
       }
     }
-    out[108 + j] = acc[j];
   }
+  const double* Lm = &sM[gg][0];
+  auto lsolve = [&](double* x) { chol6_solve_lds(Lm, x); };
+#else
+  // ---- 4. M = L L^T in every lane's registers (chol6)
+  double L[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) L[r][cc] = sM[gg][6 * r + cc];
+  chol6(L);
+  auto lsolve = [&](double* x) { chol6_solve(L, x); };
+#endif
+  // a = M^-1 (u - tau0) (every lane), dA_j = sum_{i<=j} S_i a_i, g_j = I_j dA_j,
+  // Fs_j = sum_{i>=j} g_i; then with sd = S_j x dA_j (Z_j = Zp_j + sd, y_j = yp_j + S_j x* Fs_j
+  // - IC_j sd):  dq_r += -a_r . sd (r >= j),  S_r . (S_j x* Fs_j - IC_j sd) (r < j)
+  double accj = 0.0, dA[6] = {0, 0, 0, 0, 0, 0};
+  {
+    double acc[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) acc[r] = (dyn ? X[12 + r] : 0.0) - st0[gg][r];
+    lsolve(acc);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      if (i == j) accj = acc[i];
+      if (i <= j) {
+        const double* Si = &xs[gg][i][12];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dA[r] += Si[r] * acc[i];
+      }
+    }
+  }
+  {
+    // g_j goes where e_j was (e is not read after step 3)
+    double gI[6];
+    imul(m, h, Ib, dA, gI);
+    if (g < KPW) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) my[6 + r] = gI[r];
+    }
+  }
+  wave_sync();
+  {
+    double Fs[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      if (i >= j) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) Fs[r] += xs[gg][i][6 + r];
+      }
+    }
+    double sd[6], t1[6], t2[6];
+    mcross(Sj, dA, sd);
+    imul(cm, ch, cI, sd, t1);
+    fcross(Sj, Fs, t2);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) t2[r] -= t1[r];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double* o = &xs[gg][r][0];
+      dq[r] += (r >= j) ? -dot6(o, sd) : dot6(o + 12, t2);
+    }
+  }
+
+  // ---- 5. -M^-1 of the columns and outputs, one matrix at a time (the fences make every
+  // solve re-read the factor from LDS instead of holding it in registers)
+  const double dt = P.dt;
+  const double qj = dyn ? X[j] : 0.0, vj = dyn ? X[6 + j] : 0.0, uj = dyn ? X[12 + j] : 0.0;
+  double* out = lin + ((long)(dyn ? b : 0) * (P.N - 1) + (dyn ? k : 0)) * LIN_STRIDE;
+  double part[6];  // row r of (Aq q + Av v + Bu u), lane j's column term
+  wave_sync();
+  lsolve(dq);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const double aq = -dt * dq[r];
+    if (dyn) out[6 * r + j] = aq;
+    part[r] = aq * qj;
+  }
+  wave_sync();
+  lsolve(dv);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const double av = (r == j ? 1.0 : 0.0) - dt * dv[r];
+    if (dyn) out[36 + 6 * r + j] = av;
+    part[r] += av * vj;
+  }
+  wave_sync();
+  {
+    double em[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) em[r] = (r == j) ? 1.0 : 0.0;
+    lsolve(em);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double bu = dt * em[r];
+      if (dyn && r <= j) {
+        out[72 + 6 * r + j] = bu;
+        out[72 + 6 * j + r] = bu;
+      }
+      part[r] += bu * uj;
+    }
+  }
+  if (dyn) out[108 + j] = accj;
   if (qpd) {
     // the knot's QP record for k_riccati_mfma (QPD_* layout): c_v = v + dt a - (Aq q + Av v + Bu u)
     // (src/osqp_solver.py:76-81), the linear cost terms Qm j | dQm v | Rm u (src/osqp_solver.py:
     // 121-135), j, dQm, Rm.  Row r of Aq/Av/Bu is spread over the knot's lanes (lane j owns
-    // column j): partial products go through the free tail of the LDS slot.
-    const double dt = P.dt;
-    const double qj = X[j], uj = dyn ? X[12 + j] : 0.0;
+    // column j): the partial products go through sM.
+    wave_sync();  // every lane has read the factor
     if (g < KPW) {
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const double aq = -dt * dq[r], av = (r == j ? 1.0 : 0.0) - dt * dv[r], bu = dt * em[r];
-        my[24 + r] = aq * qj + av * v[j] + bu * uj;
-      }
+      for (int r = 0; r < 6; ++r) sM[gg][6 * j + r] = part[r];
     }
     wave_sync();
     if (dyn) {
       double sacc = 0.0;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) sacc += xs[gg][i][24 + j];
+      for (int i = 0; i < 6; ++i) sacc += sM[gg][6 * i + j];
       const double qm = (k == P.N - 1) ? P.QN : 1.0;
       const double w = wreg;
       double* o = qpd + ((long)b * (P.N - 1) + k) * QPD_STRIDE;
-      o[QPD_CV + j] = (v[j] + acc[j] * dt) - sacc;
+      o[QPD_CV + j] = (vj + accj * dt) - sacc;
       o[QPD_LX + j] = qm * jte;
-      o[QPD_LX + 6 + j] = (P.dQ * w) * v[j];
+      o[QPD_LX + 6 + j] = (P.dQ * w) * vj;
       o[QPD_LU + j] = (P.R * w) * uj;
       o[QPD_J + j] = jte;
       if (j == 0) {
@@ -469,7 +600,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
 
 // KPW consecutive knots of the flattened (problem, knot) index per 64-lane wave.
 template <bool SPEC, bool FW = false>
-__global__ void __launch_bounds__(64) k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
+__global__ void __launch_bounds__(64) I7M_LIN_OCC k_linearize(const DevModel* __restrict__ Mg, SolveParams P,
                                                   const double* __restrict__ xu, const double* __restrict__ goals,
                                                   const double* __restrict__ fext, const int* __restrict__ active,
                                                   double* __restrict__ lin, double* __restrict__ cost,

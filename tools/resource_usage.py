@@ -1,7 +1,7 @@
 """Compact per-kernel resource table (VGPRs, SGPRs, spills, scratch, LDS, occupancy) of the
 library's translation units, from hipcc's -Rpass-analysis=kernel-resource-usage remarks.
 
-    python tools/resource_usage.py [filter-substring ...] [--diag]
+    python tools/resource_usage.py [filter-substring ...] [--diag] [--unit=lin_tu]
 """
 import os
 import re
@@ -29,10 +29,14 @@ def demangle(names):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     defines = ["-DI7M_DIAG"] if "--diag" in sys.argv else []
+    unit = next((a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--unit=")), "")
+    extra_flags = next((a.split("=", 1)[1].split() for a in sys.argv[1:] if a.startswith("--flags=")), [])
     rows = []
     with tempfile.TemporaryDirectory() as td:
         for i, (src, extra) in enumerate(ge.LIB_UNITS):
-            cmd = [ge.HIPCC, f"--offload-arch={ge.ARCH}", "-O3", "-std=c++17", "-fPIC", *extra, *defines,
+            if unit not in os.path.basename(src):
+                continue
+            cmd = [ge.HIPCC, f"--offload-arch={ge.ARCH}", "-O3", "-std=c++17", "-fPIC", *extra, *defines, *extra_flags,
                    "-I" + os.path.join(ROOT, "include"), "-c", src, "-o", os.path.join(td, f"u{i}.o"),
                    "-Rpass-analysis=kernel-resource-usage"]
             err = subprocess.run(cmd, capture_output=True, text=True).stderr
