@@ -59,13 +59,15 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--modes", default="fused,delta,split")
     a = ap.parse_args()
     res, outs = {}, {}
-    for mode in ("fused", "delta", "split"):
+    modes = a.modes.split(",")
+    for mode in modes:
         outs[mode], res[mode] = run(mode, a.B, a.N, a.steps)
         res[mode].pop("ipm_iters_hist")
-    ref = outs["split"]
-    for mode in ("fused", "delta"):
+    ref = outs.get("split")
+    for mode in ([m for m in ("fused", "delta") if m in modes] if ref is not None else []):
         d = outs[mode] - ref
         res[mode]["vs_split"] = {"bit_identical": bool(np.array_equal(outs[mode], ref)),
                                  "max_abs_diff": float(np.abs(d).max()),
