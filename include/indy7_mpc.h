@@ -38,6 +38,17 @@
  *   goals (B, N*goal_stride), goal_stride 3 (OSQP surface, src/osqp_solver.py:111) or
  *         6 (batch_sqp surface, gato_controller.py:180-183; first 3 of each 6 used)
  *
+ * Deviations from the C-ABI sketched in SURVEY.md §8(b):
+ *   - no ADMM mode (`qp_mode` admm): I7M_QP_DIRECT solves each SQP subproblem QP exactly (the
+ *     optimum OSQP's ADMM approximates to eps 1e-3, src/osqp_solver.py:39-41); box rows
+ *     (config 4) use an interior point whose Newton steps are the same exact solve — measured
+ *     against ADMM in DESIGN.md §4.4 (ADMM needed 40-4700 iterations on those problems);
+ *   - no `precision` field: every kernel computes in fp64.  The drop-in batch_sqp module keeps
+ *     the reference's SQPSolverfloat_* class names (gato_controller.py:54-62) so callers run
+ *     unchanged, but it also solves (and returns) fp64;
+ *   - i7m_reset exists but has little to reset: the exact solve keeps no warm start, penalty
+ *     or dual state between calls (the reference's OSQP warm start, src/osqp_solver.py:140-143).
+ *
  * Status: 0 = OK, <0 = error (see I7M_E*), message via i7m_last_error() (thread-local).
  * Threading: a handle is not re-entrant (like the reference's stateful OSQPSolver);
  * use one handle per (host thread, device).
@@ -129,6 +140,12 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out);
 void i7m_destroy(i7m_handle* h);
 /* NULL -> the handle's own stream, a blocking stream (ordered with the legacy null stream) */
 int i7m_set_stream(i7m_handle* h, void* stream);
+/* Back to the post-create solver state (batch_sqp reset / resetRho / resetLambda,
+ * gato_controller.py:132-138): waits for the handle's stream, drops captured solve graphs and
+ * zeroes the kernel timing sums.  The exact solve carries no warm start, penalty or dual state
+ * across calls, so results never depend on earlier calls either way.  The external wrench is
+ * caller input like the model and is kept: clear it with i7m_set_external_wrench(h, 0, NULL, 0). */
+int i7m_reset(i7m_handle* h);
 int i7m_synchronize(i7m_handle* h);
 
 /* External wrench [force; torque] acting on joint 6's body.  Frames:

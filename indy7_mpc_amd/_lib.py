@@ -127,6 +127,7 @@ SIGNATURES = [
     ("i7m_set_timing", C.c_int, [_H, C.c_int]),
     ("i7m_get_kernel_times", C.c_int, [_H, _DP, C.POINTER(C.c_int32), C.c_int32]),
     ("i7m_reset_kernel_times", C.c_int, [_H]),
+    ("i7m_reset", C.c_int, [_H]),
 ]
 
 _lib = None
@@ -374,3 +375,8 @@ class Handle:
 
     def reset_kernel_times(self):
         _check(self._lib.i7m_reset_kernel_times(self._h))
+
+    def reset(self):
+        """i7m_reset: back to the post-create solver state (no warm start exists to clear; drops
+        captured graphs and timing sums; the external wrench is kept)."""
+        _check(self._lib.i7m_reset(self._h))

@@ -74,13 +74,19 @@ class _SQPSolverBatch:
         }
 
     def reset(self):
-        """Warm-start state reset; the exact solve keeps no solver state between calls."""
+        """Solver state reset (i7m_reset): the exact solve keeps no warm start between calls, so
+        results are unchanged; the wrench hypotheses are kept."""
+        for h in (self._h, self._sim):
+            if h is not None:
+                h.reset()
 
     def resetRho(self):
-        """ADMM/PCG penalty reset; a no-op for the exact solve."""
+        """ADMM/PCG penalty reset: the exact solve has no penalty, so this is i7m_reset."""
+        self.reset()
 
     def resetLambda(self):
-        """Dual reset; a no-op for the exact solve."""
+        """Dual reset: the exact solve keeps no duals between calls, so this is i7m_reset."""
+        self.reset()
 
     def set_external_wrench_batch(self, f_ext_batch):
         f = np.asarray(f_ext_batch, dtype=float).reshape(self.batch_size, 6)

@@ -653,6 +653,7 @@ int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext, int32_
   if (!h) return fail(I7M_EINVAL, "null handle");
   if (!fext) {
     h->has_fext = false;
+    drop_graphs(h);  // captured graphs hold the wrench kernel choice
     return I7M_OK;
   }
   if (frame != I7M_WRENCH_LOCAL && frame != I7M_WRENCH_WORLD)
@@ -667,6 +668,14 @@ int i7m_set_external_wrench(i7m_handle* h, int32_t B, const double* fext, int32_
   // captured graphs hold the old wrench pointer / kernel choice
   drop_graphs(h);
   return I7M_OK;
+}
+
+int i7m_reset(i7m_handle* h) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  HIPCHK(hipSetDevice(h->dev));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  drop_graphs(h);
+  return i7m_reset_kernel_times(h);
 }
 
 int i7m_synchronize(i7m_handle* h) {

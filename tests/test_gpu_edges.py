@@ -163,6 +163,25 @@ def test_release_library_refuses_ablation_knob(lib, model, monkeypatch):
     lib.Handle(model, N=16).close()
 
 
+def test_reset_and_wrench_clear_with_captured_graphs(lib, model, monkeypatch):
+    """i7m_reset keeps results (the exact solve has no warm start) and the wrench; clearing the
+    wrench afterwards must not replay a graph captured with the wrench kernels (I7M_GRAPH=1)."""
+    monkeypatch.setenv("I7M_GRAPH", "1")
+    N, B = 16, 5
+    xcur, goals, XU = synthetic_batch(B, N, seed=23)
+    f = np.random.default_rng(6).normal(0, 30, (B, 6))
+    plain, _ = lib.Handle(model, N=N, max_batch=B).solve(xcur, goals, XU)
+    h = lib.Handle(model, N=N, max_batch=B)
+    h.set_external_wrench(f, "world")
+    w1, _ = h.solve(xcur, goals, XU)
+    h.reset()
+    w2, _ = h.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(w1, w2)
+    assert not np.array_equal(w1, plain)
+    h.set_external_wrench(None)
+    np.testing.assert_array_equal(h.solve(xcur, goals, XU)[0], plain)
+
+
 def test_zero_step_accepts_alpha_one(lib, model):
     """A QP minimiser equal to XU (sol == XU): the reference's merit_new == basemerit exactly, so
     alpha = 1 is accepted (src/osqp_sqp.py:58-72).  The line-search hook (base evaluated by the

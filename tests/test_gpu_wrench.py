@@ -147,6 +147,8 @@ def test_batch_sqp_surface_world_wrench(lib, model):
     h.set_external_wrench(f, "world")
     ref, _ = h.solve(xcur, goals, XU)
     np.testing.assert_array_equal(r["xu_trajectory"], ref)
+    s.reset()  # i7m_reset on the solve handle: no state to lose, the hypotheses stay
+    np.testing.assert_array_equal(s.solve(XU, DT, xcur, g6)["xu_trajectory"], ref)
     # sim_forward: one rk4 step per hypothesis, the world force converted at x (the host plant)
     u = np.full(6, 2.0)
     xn = s.sim_forward(xcur[0], u, DT)
