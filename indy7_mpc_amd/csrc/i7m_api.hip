@@ -72,6 +72,10 @@ struct Timing {
 
 }  // namespace
 
+// k_riccati_mfma's Gauss-Jordan pivot broadcasts switch from v_readlane to DPP from this batch
+// size on (riccati_mfma_body BC)
+constexpr int RIC_DPP_MIN_B = 2048;
+
 struct i7m_handle {
   i7m_config cfg;
   int dev = 0;
@@ -110,6 +114,7 @@ struct i7m_handle {
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
   int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
   int pipeline = I7M_PIPE_AUTO;  // cfg.pipeline, or I7M_PIPE=split|fused
+  int ric_bc = -1;               // k_riccati_mfma broadcast variant (BC bits), -1 = by batch size
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -277,7 +282,20 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       default: launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
     }
 #else
-    launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
+    // cross-lane broadcasts (riccati_mfma_body BC): the rollout's by DPP at every batch size; the
+    // pivots' by DPP from RIC_DPP_MIN_B problems on (fewer instructions) and by v_readlane below
+    // (shorter chain); I7M_RIC_BC=0..3 forces one (A/B)
+    const int bc = h->ric_bc >= 0 ? h->ric_bc : (P.B >= RIC_DPP_MIN_B ? 3 : 2);
+    auto go = [&](auto kern) {
+      hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
+                            sol, (const double*)nullptr, (const double*)nullptr);
+    };
+    switch (bc) {
+      case 1: go(k_riccati_mfma<0, false, 1>); break;
+      case 2: go(k_riccati_mfma<0, false, 2>); break;
+      case 3: go(k_riccati_mfma<0, false, 3>); break;
+      default: go(k_riccati_mfma<0, false, 0>);
+    }
 #endif
   });
 }
@@ -587,6 +605,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
+  if (const char* e = std::getenv("I7M_RIC_BC")) h->ric_bc = std::atoi(e) & 3;
   h->pipeline = cfg->pipeline;
   if (const char* e = std::getenv("I7M_PIPE"))
     h->pipeline = std::strcmp(e, "fused") == 0 ? I7M_PIPE_FUSED

@@ -61,6 +61,37 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// v from lane J of each 16-lane row into every lane of that row: one v_mov_b64_dpp
+// row_newbcast:J (gfx950 has 64-bit DPP for row_newbcast), the result in a VGPR.  Against
+// readlane_f64: one instruction instead of two, and no VALU-writes-SGPR hazard.
+template <int J>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false);
+}
+template <int J, int NJ>
+struct RowBcast {  // out[j] = row_bcast_f64<j>(v), j = J .. NJ-1
+  static __device__ __forceinline__ void run(double v, double* out) {
+    out[J] = row_bcast_f64<J>(v);
+    RowBcast<J + 1, NJ>::run(v, out);
+  }
+};
+template <int NJ>
+struct RowBcast<NJ, NJ> {
+  static __device__ __forceinline__ void run(double, double*) {}
+};
+// row_bcast_f64 with the source lane as an argument that is a constant after unrolling (the DPP
+// control must be an immediate: the switch folds away)
+__device__ __forceinline__ double row_bcast_f64_at(double v, const int j) {
+  switch (j) {
+    case 0: return row_bcast_f64<0>(v);
+    case 1: return row_bcast_f64<1>(v);
+    case 2: return row_bcast_f64<2>(v);
+    case 3: return row_bcast_f64<3>(v);
+    case 4: return row_bcast_f64<4>(v);
+    default: return row_bcast_f64<5>(v);
+  }
+}
+
 // lane l <- lane l + 6 within each 16-lane row (DPP row_shl:6), fp64 as two 32-bit moves
 __device__ __forceinline__ double row_shl6_f64(double v) {
   const long long bits = __double_as_longlong(v);
@@ -100,7 +131,13 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // LDS); k_riccati_mfma runs it once, k_ipm_fused (i7m_box.h) once per Newton step.
 // HINV (box predictor steps): also carry the identity through the elimination and store H^-1
 // of every stage in hinv (B, N-1, 36) for riccati_delta_body (column-per-lane elimination).
-template <int ABL, bool BOX, bool HINV = false>
+// BC: cross-lane broadcasts by DPP row_newbcast instead of v_readlane — bit 0 the Gauss-Jordan
+// pivot columns, bit 1 the rollout's x and u; bit-identical either way.  Measured (DESIGN.md
+// §4.2): bit 1 helps at every batch size; bit 0 helps at B = 4096 (fewer instructions) and
+// costs ~4.5 us per launch at B <= 256 (a longer pivot chain), so launch_riccati sets it by
+// batch size.  The config-4 body (BOX) keeps v_readlane: DPP values live in VGPRs, and its
+// fused interior-point kernel spills more with them (10.7 -> 12.2 ms per QP).
+template <int ABL, bool BOX, bool HINV = false, int BC = 0>
 __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
                                                   const double* __restrict__ xs, const double* __restrict__ lin,
                                                   const double* __restrict__ cost, const double* __restrict__ qpd,
@@ -320,9 +357,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       if (l < 6) kk[78 + l] = sh[MO_CV + l];
     } else {
-      // Column-per-lane Gauss-Jordan with v_readlane pivot broadcast (every variant by default):
-      // H, G~ through LDS, one column of [H | G~] per
-      // lane (lanes 0..18); HINV adds the identity columns in lanes 19..24, which end as H^-1.
+      // Column-per-lane Gauss-Jordan (every variant by default): H, G~ through LDS, one column
+      // of [H | G~ (| I)] per lane, the pivot column broadcast by DPP row_newbcast, which stays
+      // inside a 16-lane row — so each of the two rows used carries its own copy of H's six
+      // columns: row 0 = H 0..5, G~ 0..9; row 1 = H 0..5 again, G~ 10..12 and (HINV) the
+      // identity columns, which end as H^-1.  The two copies of H evolve identically.
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = lq + 4 * i;
@@ -333,8 +372,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       wave_sync();
       double E[6];
+      // column of lane l: 0..5 H, 6..18 G~, 19..24 identity (HINV); -1 unused (rows 2, 3 and
+      // row 1's tail compute a copy of H column 0 and store nothing)
+      const int m16 = l & 15;
       const int ncol = HINV ? 25 : 19;
-      const int cc = l < ncol ? l : ncol - 1;
+      const int cc_own = !(BC & 1) ? l
+                         : (l < 16) ? m16 : (l < 32 ? (m16 < 6 ? m16 : (m16 < (HINV ? 15 : 9) ? m16 + 10 : -1)) : -1);
+      const int cc = !(BC & 1) ? (l < ncol ? l : ncol - 1) : (cc_own < 0 ? 0 : cc_own);
 #pragma unroll
       for (int i = 0; i < 6; ++i)
         E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : (cc < 19 ? sh[MO_G + 13 * i + (cc - 6)] : (i == cc - 19 ? 1.0 : 0.0));
@@ -343,21 +387,21 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       for (int p = 0; p < 6; ++p) {
         double Pc[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) Pc[i] = readlane_f64(E[i], p);
+        for (int i = 0; i < 6; ++i) Pc[i] = (BC & 1) ? row_bcast_f64_at(E[i], p) : readlane_f64(E[i], p);
         const double inv = rcp_nr(Pc[p]);
         const double ep = E[p] * inv;
 #pragma unroll
         for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
       }
       if (ABL & 512) te = tstamp(E[0] + E[1] + E[2] + E[3] + E[4] + E[5]);
-      if (l >= 6 && l < 19) {
+      if (cc_own >= 6 && cc_own < 19) {  // (BC & 1) == 0: lane l = column l
 #pragma unroll
-        for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (l - 6)] = -E[i];
+        for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (cc_own - 6)] = -E[i];
       }
-      if (HINV && l >= 19 && l < 25) {
+      if (HINV && cc_own >= 19 && cc_own < 25) {
         double* hk = hinv + ((long)b * (N - 1) + k) * 36;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) hk[6 * i + (l - 19)] = E[i];
+        for (int i = 0; i < 6; ++i) hk[6 * i + (cc_own - 19)] = E[i];
       }
       wave_sync();
       if (ABL & 512) tm3 = tstamp(E[0]);
@@ -383,8 +427,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   }
 
   // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
-  // Lane l < 12 holds x_l and lane m < 6 holds u_m; every lane sees the full vectors through
-  // v_readlane.  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
+  // Lane l < 12 holds x_l and lane m < 6 holds u_m; the lanes of DPP row 0 see the full vectors
+  // through row_newbcast (one 64-bit DPP move per value).  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
   // (3 per lane) two stages ahead into registers and dropped into one LDS slot permuted so that
   // the 19 values each lane needs are contiguous: lane m < 6 the row m of K~ (13, then zeros),
   // lane 6 + i c_v[i] and row i of Aq, Av, Bu; lanes >= 12 an all-zero block.  Every lane then
@@ -450,9 +494,14 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
     for (int j = 0; j < 19; ++j) r[j] = myb[j];
     }
+    // x (lanes 0..11, all in DPP row 0) to every lane of the row
     double X[12];
+    if (BC & 2) {
+      RowBcast<0, 12>::run(xreg, X);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
+      for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
+    }
     // u (lanes 0..5): two partial sums to halve the dependency chain
     double ua = r[12], ub = 0.0;
 #pragma unroll
@@ -460,8 +509,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     const double ureg = ua + ub;
     if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 6) S[18 * k + 12 + l] = ureg;
     double U[6];
+    if (BC & 2) {
+      RowBcast<0, 6>::run(ureg, U);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
+      for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
+    }
     double va = r[0], vb = 0.0, vc = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -622,7 +675,7 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
   if (k < N - 1) stage(k, fa);
 }
 
-template <int ABL, bool BOX = false>
+template <int ABL, bool BOX = false, int BC = 0>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_riccati_mfma(SolveParams P, const double* __restrict__ xu,
                                                      const double* __restrict__ xs, const double* __restrict__ lin,
                                                      const double* __restrict__ cost, const double* __restrict__ qpd,
@@ -634,7 +687,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   if (b >= P.B) return;
   if (active && !active[b]) return;
   __shared__ double sh[MO_TOTAL];
-  riccati_mfma_body<ABL, BOX>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, bsig, bh, sh, threadIdx.x);
+  riccati_mfma_body<ABL, BOX, false, BC>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, bsig, bh, sh, threadIdx.x);
 }
 
 }  // namespace i7m
