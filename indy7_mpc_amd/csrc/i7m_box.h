@@ -463,7 +463,7 @@ k_ipm_fused(IpmFusedArgs args) {
     const SolveParams P = A->P;
     __syncthreads();
     if (!DELTA) {
-      riccati_mfma_body<0, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l);
+      riccati_mfma_body<0, true, false, 2>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l);
     } else if (half == 0) {
       riccati_mfma_body<0, true, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
                                        A->hinv);

@@ -135,8 +135,9 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // pivot columns, bit 1 the rollout's x and u; bit-identical either way.  Measured (DESIGN.md
 // §4.2): bit 1 helps at every batch size; bit 0 helps at B = 4096 (fewer instructions) and
 // costs ~4.5 us per launch at B <= 256 (a longer pivot chain), so launch_riccati sets it by
-// batch size.  The config-4 body (BOX) keeps v_readlane: DPP values live in VGPRs, and its
-// fused interior-point kernel spills more with them (10.7 -> 12.2 ms per QP).
+// batch size.  The config-4 body (BOX, k_ipm_fused) takes bit 1 only: with DPP pivots its
+// fused interior-point kernel spills more (10.7 -> 12.2 ms per QP); the DPP rollout alone
+// gives 10.68 -> 10.60 ms.
 template <int ABL, bool BOX, bool HINV = false, int BC = 0>
 __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
                                                   const double* __restrict__ xs, const double* __restrict__ lin,
