@@ -21,7 +21,10 @@
 // (g, j) owns link j of knot g.  The serial kinematic chain (~600 flops) is recomputed by every
 // link-lane; the per-link work (world inertia, its rate, forces, subtree sums, one column of the
 // derivative matrices and of M^-1) is split across the lanes; the lanes of a knot exchange
-// per-link vectors through LDS.  The terminal knot of each problem only evaluates the cost.
+// per-link vectors through LDS in three rounds of <= 19 doubles per lane (inertias and rates;
+// momenta and bias forces; a_j, e_j, S_j), each consumed as soon as it lands, and everything
+// that does not need the joint accelerations is formed before M is factorised, so the register
+// peak stays low.  The terminal knot of each problem only evaluates the cost.
 #pragma once
 
 #include "i7m_kernels.h"
