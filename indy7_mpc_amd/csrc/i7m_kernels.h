@@ -437,8 +437,11 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   }
 }
 
+#ifndef I7M_LS_WPE
+#define I7M_LS_WPE 2  // waves per SIMD the line search is compiled for (A/B builds: 3)
+#endif
 template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(2, 2))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(I7M_LS_WPE, I7M_LS_WPE))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
                                                    const double* xu, double* xu_out, const double* __restrict__ sol,
                                                    const double* __restrict__ goals, const double* __restrict__ fext,
                                                    int* __restrict__ active,
