@@ -23,6 +23,7 @@ struct BoxParams {
   double tol;
   double theta;   // initial interior margin, fraction of the box width
   double eta;     // step-to-boundary fraction
+  double z0;      // centred start: z_l = z0 / s_l, z_u = z0 / s_u, so mu_0 = z0
 };
 
 struct IpmState {
@@ -105,7 +106,8 @@ __device__ __forceinline__ double ratio_min(double t, double v, double dv) {
 // k_ipm_init / k_ipm_pred / k_ipm_corr launch them one at a time (I7M_IPM=split), and
 // k_ipm_fused runs the whole iteration of one problem in one wave.
 
-// x = clip(x_eq) into the interior, z = 1, mu, and the first predictor's Sigma and h.
+// x = clip(x_eq) into the interior, the centred duals z = z0 / s, mu, and the first predictor's
+// Sigma and h.
 __device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveParams& P, const BoxParams& BP, const int b,
                                                   const double* __restrict__ xeq, double* __restrict__ x,
                                                   double* __restrict__ zl, double* __restrict__ zu,
@@ -115,19 +117,20 @@ __device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveP
   double acc = 0.0;
   int nb = 0;
   for (int e = l; e < P.T; e += 64) {
-    double lo, hi, xv = xeq[o + e], z = 0.0, s = 0.0;
+    double lo, hi, xv = xeq[o + e], a = 0.0, c = 0.0, s = 0.0;
     if (box_of(Bt, e, lo, hi)) {
       const double w = hi - lo;
       xv = fmin(fmax(xv, lo + BP.theta * w), hi - BP.theta * w);
-      z = 1.0;
       const double sl = xv - lo, su = hi - xv;
-      acc += sl + su;
-      s = 1.0 / sl + 1.0 / su;
+      a = BP.z0 / sl;
+      c = BP.z0 / su;
+      acc += sl * a + su * c;
+      s = a / sl + c / su;
       ++nb;
     }
     x[o + e] = xv;
-    zl[o + e] = z;
-    zu[o + e] = z;
+    zl[o + e] = a;
+    zu[o + e] = c;
     sig[o + e] = s;
     h[o + e] = -s * xv;
   }

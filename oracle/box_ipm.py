@@ -15,7 +15,10 @@ whose Newton systems keep the dynamics rows exact.  This file is the restatement
 path (k_ipm_* + k_riccati_mfma<BOX>) follows step by step:
 
   init      x = clip(x_eq, lo + theta (hi - lo), hi - theta (hi - lo)) on bounded variables,
-            x_eq = the equality-only QP solution; z_l = z_u = 1.
+            x_eq = the equality-only QP solution; z_l = z0 / s_l, z_u = z0 / s_u (a centred
+            start: every complementarity product equals z0, so mu_0 = z0).  theta = 0.2 and
+            z0 = 0.1 take 6.9 iterations per config-4 QP against 12.2 for theta = 0.01, z = 1
+            (oracle/studies/ipm_iters.py).
   iterate   Sigma = z_l / s_l + z_u / s_u        (s_l = x - lo, s_u = hi - x)
             each Newton step is the equality-constrained QP
                 min 1/2 y'(P + Sigma) y + l'y   s.t.  A y = b
@@ -78,7 +81,7 @@ def _ratio(v, dv, bm):
     return float(min(1.0, np.min(-v[neg] / dv[neg])))
 
 
-def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.01, eta=0.99) -> IPMResult:
+def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, eta=0.99, z0=0.1) -> IPMResult:
     """Mehrotra predictor-corrector on the box-constrained QP (module docstring)."""
     n = len(g)
     nb = int(bm.sum())
@@ -87,8 +90,8 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.01, e
         return IPMResult(x, np.zeros(n), np.zeros(n), 0, True)
     w = np.where(bm, hi - lo, 0.0)
     x[bm] = np.clip(x_eq[bm], (lo + theta * w)[bm], (hi - theta * w)[bm])
-    zl = np.where(bm, 1.0, 0.0)
-    zu = np.where(bm, 1.0, 0.0)
+    zl = np.where(bm, z0 / np.where(bm, x - lo, 1.0), 0.0)
+    zu = np.where(bm, z0 / np.where(bm, hi - x, 1.0), 0.0)
     K0 = bmat([[Pf, A.T], [A, None]], format="csc")
     res = IPMResult(x, zl, zu, 0, False)
     rfrac = 1.0
