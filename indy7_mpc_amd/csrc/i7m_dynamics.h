@@ -83,27 +83,75 @@ template <class T> __device__ __forceinline__ T cst(double x);
 template <> __device__ __forceinline__ double cst<double>(double x) { return x; }
 template <> __device__ __forceinline__ dual cst<dual>(double x) { return dual{x, 0.0}; }
 
+// ---------------------------------------------------------------- compile-time zeros
+// With the Indy7 model baked in (kIndy7Model) many factors are exact zeros once the loops are
+// unrolled: the identity joint rotations Rp_0 / Rp_2 and the zero entries of the other Rp_i,
+// the zero components of t_i and of gravity, RNEA's qdd = 0, the base's zero velocity.  Strict
+// IEEE forbids the compiler to drop 0 * x (NaN for x = inf) or x + 0 (the sign of -0), so it
+// kept ~8 % of k_linesearch's fp64 instructions as products with a zero operand.  These
+// helpers drop a term whose factor is a compile-time 0.0 (clang's __builtin_constant_p, resolved
+// after inlining and unrolling; a dropped term's zero folds into the next helper) and are the
+// plain expression, in the original evaluation order, for every runtime operand.  For finite
+// operands the values are unchanged (up to the sign of a zero).  Measured: DESIGN.md §7.
+__device__ __forceinline__ bool kz(double x) { return __builtin_constant_p(x) && x == 0.0; }
+__device__ __forceinline__ bool kz(const dual&) { return false; }
+template <class A, class B>
+__device__ __forceinline__ auto kmul(const A& a, const B& b) {  // a b
+  using R = decltype(a * b);
+  if (kz(a) || kz(b)) return zero<R>();
+  return R(a * b);
+}
+template <class T>
+__device__ __forceinline__ T kadd(const T& a, const T& b) {  // a + b
+  if (kz(b)) return a;
+  if (kz(a)) return b;
+  return a + b;
+}
+template <class T>
+__device__ __forceinline__ T ksub(const T& a, const T& b) {  // a - b
+  if (kz(b)) return a;
+  if (kz(a)) return -b;
+  return a - b;
+}
+template <class T, class A, class B>
+__device__ __forceinline__ T kmadd(const T& s, const A& a, const B& b) {  // s + a b
+  if (kz(a) || kz(b)) return s;
+  if (kz(s)) return T(a * b);
+  return s + a * b;
+}
+template <class T, class A, class B>
+__device__ __forceinline__ T kmsub(const T& s, const A& a, const B& b) {  // s - a b
+  if (kz(a) || kz(b)) return s;
+  if (kz(s)) return -T(a * b);
+  return s - a * b;
+}
+// a0 b0 + a1 b1 + a2 b2, left to right
+template <class A, class B>
+__device__ __forceinline__ auto kdot3(const A& a0, const B& b0, const A& a1, const B& b1, const A& a2, const B& b2) {
+  return kmadd(kmadd(kmul(a0, b0), a1, b1), a2, b2);
+}
+
 // a x b
 template <class T>
 __device__ __forceinline__ void cross3(const T a[3], const T b[3], T o[3]) {
-  o[0] = a[1] * b[2] - a[2] * b[1];
-  o[1] = a[2] * b[0] - a[0] * b[2];
-  o[2] = a[0] * b[1] - a[1] * b[0];
+  o[0] = kmsub(kmul(a[1], b[2]), a[2], b[1]);
+  o[1] = kmsub(kmul(a[2], b[0]), a[0], b[2]);
+  o[2] = kmsub(kmul(a[0], b[1]), a[1], b[0]);
 }
 
 // y = Rp^T x   (Rp constant, row-major)
 template <class T>
 __device__ __forceinline__ void rpT(const double* R, const T x[3], T y[3]) {
-  y[0] = R[0] * x[0] + R[3] * x[1] + R[6] * x[2];
-  y[1] = R[1] * x[0] + R[4] * x[1] + R[7] * x[2];
-  y[2] = R[2] * x[0] + R[5] * x[1] + R[8] * x[2];
+  y[0] = kdot3(R[0], x[0], R[3], x[1], R[6], x[2]);
+  y[1] = kdot3(R[1], x[0], R[4], x[1], R[7], x[2]);
+  y[2] = kdot3(R[2], x[0], R[5], x[1], R[8], x[2]);
 }
 // y = Rp x
 template <class T>
 __device__ __forceinline__ void rp(const double* R, const T x[3], T y[3]) {
-  y[0] = R[0] * x[0] + R[1] * x[1] + R[2] * x[2];
-  y[1] = R[3] * x[0] + R[4] * x[1] + R[5] * x[2];
-  y[2] = R[6] * x[0] + R[7] * x[1] + R[8] * x[2];
+  y[0] = kdot3(R[0], x[0], R[1], x[1], R[2], x[2]);
+  y[1] = kdot3(R[3], x[0], R[4], x[1], R[5], x[2]);
+  y[2] = kdot3(R[6], x[0], R[7], x[1], R[8], x[2]);
 }
 
 // Spatial inertia (about joint origin) times motion (l, w): lin = m l - h x w, ang = Io w + h x l
@@ -113,12 +161,12 @@ __device__ __forceinline__ void inertia_mul(const DevModel& M, int i, const T l[
   const double m = M.m[i];
   const double* h = M.h[i];
   const double* I = M.Io[i];
-  fl[0] = m * l[0] - (h[1] * w[2] - h[2] * w[1]);
-  fl[1] = m * l[1] - (h[2] * w[0] - h[0] * w[2]);
-  fl[2] = m * l[2] - (h[0] * w[1] - h[1] * w[0]);
-  fn[0] = I[0] * w[0] + I[1] * w[1] + I[2] * w[2] + (h[1] * l[2] - h[2] * l[1]);
-  fn[1] = I[1] * w[0] + I[3] * w[1] + I[4] * w[2] + (h[2] * l[0] - h[0] * l[2]);
-  fn[2] = I[2] * w[0] + I[4] * w[1] + I[5] * w[2] + (h[0] * l[1] - h[1] * l[0]);
+  fl[0] = ksub(kmul(m, l[0]), kmsub(kmul(h[1], w[2]), h[2], w[1]));
+  fl[1] = ksub(kmul(m, l[1]), kmsub(kmul(h[2], w[0]), h[0], w[2]));
+  fl[2] = ksub(kmul(m, l[2]), kmsub(kmul(h[0], w[1]), h[1], w[0]));
+  fn[0] = kadd(kdot3(I[0], w[0], I[1], w[1], I[2], w[2]), kmsub(kmul(h[1], l[2]), h[2], l[1]));
+  fn[1] = kadd(kdot3(I[1], w[0], I[3], w[1], I[4], w[2]), kmsub(kmul(h[2], l[0]), h[0], l[2]));
+  fn[2] = kadd(kdot3(I[2], w[0], I[4], w[1], I[5], w[2]), kmsub(kmul(h[0], l[1]), h[1], l[0]));
 }
 
 // LDS parking of RNEA link forces (NLDS > 0, T = double only): element (link i, component k)
@@ -150,32 +198,32 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
     T tw[3], x[3], y[3];
     T tt[3] = {cst<T>(t[0]), cst<T>(t[1]), cst<T>(t[2])};
     cross3(tt, vw, tw);
-    x[0] = vl[0] - tw[0]; x[1] = vl[1] - tw[1]; x[2] = vl[2] - tw[2];
+    x[0] = ksub(vl[0], tw[0]); x[1] = ksub(vl[1], tw[1]); x[2] = ksub(vl[2], tw[2]);
     rpT(R, x, y);
-    vl[0] = c[i] * y[0] + s[i] * y[1];
-    vl[1] = c[i] * y[1] - s[i] * y[0];
+    vl[0] = kmadd(kmul(c[i], y[0]), s[i], y[1]);
+    vl[1] = kmsub(kmul(c[i], y[1]), s[i], y[0]);
     vl[2] = y[2];
     rpT(R, vw, y);
-    vw[0] = c[i] * y[0] + s[i] * y[1];
-    vw[1] = c[i] * y[1] - s[i] * y[0];
+    vw[0] = kmadd(kmul(c[i], y[0]), s[i], y[1]);
+    vw[1] = kmsub(kmul(c[i], y[1]), s[i], y[0]);
     vw[2] = y[2];
     cross3(tt, aw, tw);
-    x[0] = al[0] - tw[0]; x[1] = al[1] - tw[1]; x[2] = al[2] - tw[2];
+    x[0] = ksub(al[0], tw[0]); x[1] = ksub(al[1], tw[1]); x[2] = ksub(al[2], tw[2]);
     rpT(R, x, y);
-    al[0] = c[i] * y[0] + s[i] * y[1];
-    al[1] = c[i] * y[1] - s[i] * y[0];
+    al[0] = kmadd(kmul(c[i], y[0]), s[i], y[1]);
+    al[1] = kmsub(kmul(c[i], y[1]), s[i], y[0]);
     al[2] = y[2];
     rpT(R, aw, y);
-    aw[0] = c[i] * y[0] + s[i] * y[1];
-    aw[1] = c[i] * y[1] - s[i] * y[0];
+    aw[0] = kmadd(kmul(c[i], y[0]), s[i], y[1]);
+    aw[1] = kmsub(kmul(c[i], y[1]), s[i], y[0]);
     aw[2] = y[2];
     // joint motion: v += S qd ; a += S qdd + v x (S qd)
-    vw[2] = vw[2] + qd[i];
-    al[0] = al[0] + vl[1] * qd[i];
-    al[1] = al[1] - vl[0] * qd[i];
-    aw[0] = aw[0] + vw[1] * qd[i];
-    aw[1] = aw[1] - vw[0] * qd[i];
-    aw[2] = aw[2] + qdd[i];
+    vw[2] = kadd(vw[2], qd[i]);
+    al[0] = kmadd(al[0], vl[1], qd[i]);
+    al[1] = kmsub(al[1], vl[0], qd[i]);
+    aw[0] = kmadd(aw[0], vw[1], qd[i]);
+    aw[1] = kmsub(aw[1], vw[0], qd[i]);
+    aw[2] = kadd(aw[2], qdd[i]);
     // f = I a + v x* (I v)
     T hl[3], hn[3], il[3], in_[3], t1[3], t2[3], t3[3];
     inertia_mul(M, i, vl, vw, hl, hn);
@@ -184,8 +232,10 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
     cross3(vw, hn, t2);
     cross3(vl, hl, t3);
     T fi[6];
-    fi[0] = il[0] + t1[0]; fi[1] = il[1] + t1[1]; fi[2] = il[2] + t1[2];
-    fi[3] = in_[0] + t2[0] + t3[0]; fi[4] = in_[1] + t2[1] + t3[1]; fi[5] = in_[2] + t2[2] + t3[2];
+    fi[0] = kadd(il[0], t1[0]); fi[1] = kadd(il[1], t1[1]); fi[2] = kadd(il[2], t1[2]);
+    fi[3] = kadd(kadd(in_[0], t2[0]), t3[0]);
+    fi[4] = kadd(kadd(in_[1], t2[1]), t3[1]);
+    fi[5] = kadd(kadd(in_[2], t2[2]), t3[2]);
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       if (i < NLDS) lds_put<T>(fs + (6 * i + k) * 64, fi[k]);
@@ -225,12 +275,12 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
       const double* t = M.tp[i];
       // child -> parent: F = Rp Rz f ; N = Rp Rz n + t x F
       T x[3], F[3], Nn[3], tF[3];
-      x[0] = c[i] * f[i][0] - s[i] * f[i][1];
-      x[1] = s[i] * f[i][0] + c[i] * f[i][1];
+      x[0] = kmsub(kmul(c[i], f[i][0]), s[i], f[i][1]);
+      x[1] = kmadd(kmul(s[i], f[i][0]), c[i], f[i][1]);
       x[2] = f[i][2];
       rp(R, x, F);
-      x[0] = c[i] * f[i][3] - s[i] * f[i][4];
-      x[1] = s[i] * f[i][3] + c[i] * f[i][4];
+      x[0] = kmsub(kmul(c[i], f[i][3]), s[i], f[i][4]);
+      x[1] = kmadd(kmul(s[i], f[i][3]), c[i], f[i][4]);
       x[2] = f[i][5];
       rp(R, x, Nn);
       T tt[3] = {cst<T>(t[0]), cst<T>(t[1]), cst<T>(t[2])};
@@ -240,16 +290,16 @@ __device__ __forceinline__ void rnea(const DevModel& M, const T c[6], const T s[
         f[i - 1][0] = F[0];
         f[i - 1][1] = F[1];
         f[i - 1][2] = F[2];
-        f[i - 1][3] = Nn[0] + tF[0];
-        f[i - 1][4] = Nn[1] + tF[1];
-        f[i - 1][5] = Nn[2] + tF[2];
+        f[i - 1][3] = kadd(Nn[0], tF[0]);
+        f[i - 1][4] = kadd(Nn[1], tF[1]);
+        f[i - 1][5] = kadd(Nn[2], tF[2]);
       } else {
-        f[i - 1][0] = f[i - 1][0] + F[0];
-        f[i - 1][1] = f[i - 1][1] + F[1];
-        f[i - 1][2] = f[i - 1][2] + F[2];
-        f[i - 1][3] = f[i - 1][3] + Nn[0] + tF[0];
-        f[i - 1][4] = f[i - 1][4] + Nn[1] + tF[1];
-        f[i - 1][5] = f[i - 1][5] + Nn[2] + tF[2];
+        f[i - 1][0] = kadd(f[i - 1][0], F[0]);
+        f[i - 1][1] = kadd(f[i - 1][1], F[1]);
+        f[i - 1][2] = kadd(f[i - 1][2], F[2]);
+        f[i - 1][3] = kadd(kadd(f[i - 1][3], Nn[0]), tF[0]);
+        f[i - 1][4] = kadd(kadd(f[i - 1][4], Nn[1]), tF[1]);
+        f[i - 1][5] = kadd(kadd(f[i - 1][5], Nn[2]), tF[2]);
       }
     }
   }
@@ -274,17 +324,17 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
       const double* R = Md.Rp[j];
       const double* t = Md.tp[j];
       double x[3], F[3], Nn[3];
-      x[0] = c[j] * fl[0] - s[j] * fl[1];
-      x[1] = s[j] * fl[0] + c[j] * fl[1];
+      x[0] = kmsub(kmul(c[j], fl[0]), s[j], fl[1]);
+      x[1] = kmadd(kmul(s[j], fl[0]), c[j], fl[1]);
       x[2] = fl[2];
       rp(R, x, F);
-      x[0] = c[j] * fn[0] - s[j] * fn[1];
-      x[1] = s[j] * fn[0] + c[j] * fn[1];
+      x[0] = kmsub(kmul(c[j], fn[0]), s[j], fn[1]);
+      x[1] = kmadd(kmul(s[j], fn[0]), c[j], fn[1]);
       x[2] = fn[2];
       rp(R, x, Nn);
-      fn[0] = Nn[0] + (t[1] * F[2] - t[2] * F[1]);
-      fn[1] = Nn[1] + (t[2] * F[0] - t[0] * F[2]);
-      fn[2] = Nn[2] + (t[0] * F[1] - t[1] * F[0]);
+      fn[0] = kadd(Nn[0], kmsub(kmul(t[1], F[2]), t[2], F[1]));
+      fn[1] = kadd(Nn[1], kmsub(kmul(t[2], F[0]), t[0], F[2]));
+      fn[2] = kadd(Nn[2], kmsub(kmul(t[0], F[1]), t[1], F[0]));
       fl[0] = F[0]; fl[1] = F[1]; fl[2] = F[2];
       Mq[i][j - 1] = fn[2];
       Mq[j - 1][i] = fn[2];
@@ -294,7 +344,7 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
       const double* R = Md.Rp[i];
       const double* t = Md.tp[i];
       const double m = cm;
-      double hz[3] = {c[i] * ch[0] - s[i] * ch[1], s[i] * ch[0] + c[i] * ch[1], ch[2]};
+      double hz[3] = {kmsub(kmul(c[i], ch[0]), s[i], ch[1]), kmadd(kmul(s[i], ch[0]), c[i], ch[1]), ch[2]};
       double hr[3];
       rp(R, hz, hr);
       const double* I = cI;
@@ -311,13 +361,13 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) RA[r][q] = R[3 * r] * A[0][q] + R[3 * r + 1] * A[1][q] + R[3 * r + 2] * A[2][q];
+        for (int q = 0; q < 3; ++q) RA[r][q] = kdot3(R[3 * r], A[0][q], R[3 * r + 1], A[1][q], R[3 * r + 2], A[2][q]);
       double Bm[3][3];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int q = r; q < 3; ++q) Bm[r][q] = RA[r][0] * R[3 * q] + RA[r][1] * R[3 * q + 1] + RA[r][2] * R[3 * q + 2];
-      const double ht = hr[0] * t[0] + hr[1] * t[1] + hr[2] * t[2];
+        for (int q = r; q < 3; ++q) Bm[r][q] = kdot3(RA[r][0], R[3 * q], RA[r][1], R[3 * q + 1], RA[r][2], R[3 * q + 2]);
+      const double ht = kdot3(hr[0], t[0], hr[1], t[1], hr[2], t[2]);
       const double tt = t[0] * t[0] + t[1] * t[1] + t[2] * t[2];
       const double dg = 2.0 * ht + m * tt;
       const int iu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
@@ -325,15 +375,15 @@ __device__ __forceinline__ void crba(const DevModel& Md, const double c[6], cons
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         const int r = iu[k][0], q = iu[k][1];
-        double v = Bm[r][q] - (t[r] * hr[q] + hr[r] * t[q]) - m * t[r] * t[q];
+        double v = ksub(ksub(Bm[r][q], kmadd(kmul(t[r], hr[q]), hr[r], t[q])), kmul(kmul(m, t[r]), t[q]));
         if (r == q) v += dg;
         nI[k] = Md.Io[i - 1][k] + v;
       }
 #pragma unroll
       for (int k = 0; k < 6; ++k) cI[k] = nI[k];
-      ch[0] = Md.h[i - 1][0] + (hr[0] + m * t[0]);
-      ch[1] = Md.h[i - 1][1] + (hr[1] + m * t[1]);
-      ch[2] = Md.h[i - 1][2] + (hr[2] + m * t[2]);
+      ch[0] = kadd(Md.h[i - 1][0], kmadd(hr[0], m, t[0]));
+      ch[1] = kadd(Md.h[i - 1][1], kmadd(hr[1], m, t[1]));
+      ch[2] = kadd(Md.h[i - 1][2], kmadd(hr[2], m, t[2]));
       cm = Md.m[i - 1] + m;
     }
   }
@@ -425,12 +475,12 @@ __device__ __forceinline__ void fk_pos(const DevModel& Md, const double c[6], co
   double w[3] = {Md.tp[5][0], Md.tp[5][1], Md.tp[5][2]};
 #pragma unroll
   for (int i = 4; i >= 0; --i) {
-    const double x[3] = {c[i] * w[0] - s[i] * w[1], s[i] * w[0] + c[i] * w[1], w[2]};
+    const double x[3] = {kmsub(kmul(c[i], w[0]), s[i], w[1]), kmadd(kmul(s[i], w[0]), c[i], w[1]), w[2]};
     double y[3];
     rp(Md.Rp[i], x, y);
-    w[0] = Md.tp[i][0] + y[0];
-    w[1] = Md.tp[i][1] + y[1];
-    w[2] = Md.tp[i][2] + y[2];
+    w[0] = kadd(Md.tp[i][0], y[0]);
+    w[1] = kadd(Md.tp[i][1], y[1]);
+    w[2] = kadd(Md.tp[i][2], y[2]);
   }
   p[0] = w[0];
   p[1] = w[1];
@@ -452,15 +502,15 @@ __device__ __forceinline__ void wrench_world_to_local(const DevModel& Md, const 
     const double* t = Md.tp[i];
     double np_[3], RR[3][3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[r][0] * t[0] + R[r][1] * t[1] + R[r][2] * t[2];
+    for (int r = 0; r < 3; ++r) np_[r] = kmadd(kmadd(kmadd(p[r], R[r][0], t[0]), R[r][1], t[1]), R[r][2], t[2]);
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) RR[r][q] = R[r][0] * Rp[q] + R[r][1] * Rp[3 + q] + R[r][2] * Rp[6 + q];
+      for (int q = 0; q < 3; ++q) RR[r][q] = kdot3(R[r][0], Rp[q], R[r][1], Rp[3 + q], R[r][2], Rp[6 + q]);
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      R[r][0] = RR[r][0] * c[i] + RR[r][1] * s[i];
-      R[r][1] = RR[r][1] * c[i] - RR[r][0] * s[i];
+      R[r][0] = kmadd(kmul(RR[r][0], c[i]), RR[r][1], s[i]);
+      R[r][1] = kmsub(kmul(RR[r][1], c[i]), RR[r][0], s[i]);
       R[r][2] = RR[r][2];
       p[r] = np_[r];
     }
@@ -471,8 +521,8 @@ __device__ __forceinline__ void wrench_world_to_local(const DevModel& Md, const 
   const double m2 = fw[5] - (p[0] * f1 - p[1] * f0);
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    fl[q] = R[0][q] * f0 + R[1][q] * f1 + R[2][q] * f2;
-    fl[3 + q] = R[0][q] * m0 + R[1][q] * m1 + R[2][q] * m2;
+    fl[q] = kdot3(R[0][q], f0, R[1][q], f1, R[2][q], f2);
+    fl[3 + q] = kdot3(R[0][q], m0, R[1][q], m1, R[2][q], m2);
   }
 }
 
@@ -490,18 +540,18 @@ __device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], co
     const double* t = Md.tp[i];
     double np[3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) np[r] = pos[r] + R[r][0] * t[0] + R[r][1] * t[1] + R[r][2] * t[2];
+    for (int r = 0; r < 3; ++r) np[r] = kmadd(kmadd(kmadd(pos[r], R[r][0], t[0]), R[r][1], t[1]), R[r][2], t[2]);
     // R <- R Rp Rz(q)
     double RR[3][3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) RR[r][q] = R[r][0] * Rp[q] + R[r][1] * Rp[3 + q] + R[r][2] * Rp[6 + q];
+      for (int q = 0; q < 3; ++q) RR[r][q] = kdot3(R[r][0], Rp[q], R[r][1], Rp[3 + q], R[r][2], Rp[6 + q]);
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       const double x0 = RR[r][0], x1 = RR[r][1];
-      R[r][0] = x0 * c[i] + x1 * s[i];
-      R[r][1] = x1 * c[i] - x0 * s[i];
+      R[r][0] = kmadd(kmul(x0, c[i]), x1, s[i]);
+      R[r][1] = kmsub(kmul(x1, c[i]), x0, s[i]);
       R[r][2] = RR[r][2];
       zs[i][r] = RR[r][2];
       ps[i][r] = np[r];
@@ -512,10 +562,10 @@ __device__ __forceinline__ void fk_jac(const DevModel& Md, const double c[6], co
   if (J) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const double d0 = pos[0] - ps[j][0], d1 = pos[1] - ps[j][1], d2 = pos[2] - ps[j][2];
-      J[0][j] = zs[j][1] * d2 - zs[j][2] * d1;
-      J[1][j] = zs[j][2] * d0 - zs[j][0] * d2;
-      J[2][j] = zs[j][0] * d1 - zs[j][1] * d0;
+      const double d0 = ksub(pos[0], ps[j][0]), d1 = ksub(pos[1], ps[j][1]), d2 = ksub(pos[2], ps[j][2]);
+      J[0][j] = kmsub(kmul(zs[j][1], d2), zs[j][2], d1);
+      J[1][j] = kmsub(kmul(zs[j][2], d0), zs[j][0], d2);
+      J[2][j] = kmsub(kmul(zs[j][0], d1), zs[j][1], d0);
     }
   }
 }

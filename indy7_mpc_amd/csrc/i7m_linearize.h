@@ -55,12 +55,12 @@ constexpr int XS = 20;    // LDS doubles per link slot (round 1 uses 19)
 
 // spatial helpers on 6-vectors [lin; ang]
 __device__ __forceinline__ void mcross(const double* a, const double* b, double* o) {  // a x b (motion)
-  o[0] = a[4] * b[2] - a[5] * b[1] + a[1] * b[5] - a[2] * b[4];
-  o[1] = a[5] * b[0] - a[3] * b[2] + a[2] * b[3] - a[0] * b[5];
-  o[2] = a[3] * b[1] - a[4] * b[0] + a[0] * b[4] - a[1] * b[3];
-  o[3] = a[4] * b[5] - a[5] * b[4];
-  o[4] = a[5] * b[3] - a[3] * b[5];
-  o[5] = a[3] * b[4] - a[4] * b[3];
+  o[0] = kmsub(kmadd(kmsub(kmul(a[4], b[2]), a[5], b[1]), a[1], b[5]), a[2], b[4]);
+  o[1] = kmsub(kmadd(kmsub(kmul(a[5], b[0]), a[3], b[2]), a[2], b[3]), a[0], b[5]);
+  o[2] = kmsub(kmadd(kmsub(kmul(a[3], b[1]), a[4], b[0]), a[0], b[4]), a[1], b[3]);
+  o[3] = kmsub(kmul(a[4], b[5]), a[5], b[4]);
+  o[4] = kmsub(kmul(a[5], b[3]), a[3], b[5]);
+  o[5] = kmsub(kmul(a[3], b[4]), a[4], b[3]);
 }
 __device__ __forceinline__ void fcross(const double* m, const double* f, double* o) {  // m x* f
   o[0] = m[4] * f[2] - m[5] * f[1];
@@ -75,12 +75,12 @@ __device__ __forceinline__ double dot6(const double* a, const double* b) {
 }
 // inertia (m, h[3], I[6] sym xx xy xz yy yz zz, about the world origin) times motion x
 __device__ __forceinline__ void imul(double m, const double* h, const double* I, const double* x, double* o) {
-  o[0] = m * x[0] - (h[1] * x[5] - h[2] * x[4]);
-  o[1] = m * x[1] - (h[2] * x[3] - h[0] * x[5]);
-  o[2] = m * x[2] - (h[0] * x[4] - h[1] * x[3]);
-  o[3] = I[0] * x[3] + I[1] * x[4] + I[2] * x[5] + (h[1] * x[2] - h[2] * x[1]);
-  o[4] = I[1] * x[3] + I[3] * x[4] + I[4] * x[5] + (h[2] * x[0] - h[0] * x[2]);
-  o[5] = I[2] * x[3] + I[4] * x[4] + I[5] * x[5] + (h[0] * x[1] - h[1] * x[0]);
+  o[0] = ksub(kmul(m, x[0]), kmsub(kmul(h[1], x[5]), h[2], x[4]));
+  o[1] = ksub(kmul(m, x[1]), kmsub(kmul(h[2], x[3]), h[0], x[5]));
+  o[2] = ksub(kmul(m, x[2]), kmsub(kmul(h[0], x[4]), h[1], x[3]));
+  o[3] = kadd(kdot3(I[0], x[3], I[1], x[4], I[2], x[5]), kmsub(kmul(h[1], x[2]), h[2], x[1]));
+  o[4] = kadd(kdot3(I[1], x[3], I[3], x[4], I[4], x[5]), kmsub(kmul(h[2], x[0]), h[0], x[2]));
+  o[5] = kadd(kdot3(I[2], x[3], I[4], x[4], I[5], x[5]), kmsub(kmul(h[0], x[1]), h[1], x[0]));
 }
 
 // Solve L L^T x = b in place, L from chol6's layout (strict lower triangle = L, diagonal =
@@ -169,30 +169,31 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
         const double* t = Md.tp[i];
         double np_[3], RR[9];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) np_[r] = p[r] + R[3 * r] * t[0] + R[3 * r + 1] * t[1] + R[3 * r + 2] * t[2];
+        for (int r = 0; r < 3; ++r)
+          np_[r] = kmadd(kmadd(kmadd(p[r], R[3 * r], t[0]), R[3 * r + 1], t[1]), R[3 * r + 2], t[2]);
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
-          for (int qq = 0; qq < 3; ++qq) RR[3 * r + qq] = R[3 * r] * Rp[qq] + R[3 * r + 1] * Rp[3 + qq] + R[3 * r + 2] * Rp[6 + qq];
+          for (int qq = 0; qq < 3; ++qq) RR[3 * r + qq] = kdot3(R[3 * r], Rp[qq], R[3 * r + 1], Rp[3 + qq], R[3 * r + 2], Rp[6 + qq]);
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-          R[3 * r] = RR[3 * r] * c[i] + RR[3 * r + 1] * s[i];
-          R[3 * r + 1] = RR[3 * r + 1] * c[i] - RR[3 * r] * s[i];
+          R[3 * r] = kmadd(kmul(RR[3 * r], c[i]), RR[3 * r + 1], s[i]);
+          R[3 * r + 1] = kmsub(kmul(RR[3 * r + 1], c[i]), RR[3 * r], s[i]);
           R[3 * r + 2] = RR[3 * r + 2];
           p[r] = np_[r];
         }
         // S = (p x z; z), z = R[:,2]
         double S[6];
         S[3] = R[2]; S[4] = R[5]; S[5] = R[8];
-        S[0] = p[1] * S[5] - p[2] * S[4];
-        S[1] = p[2] * S[3] - p[0] * S[5];
-        S[2] = p[0] * S[4] - p[1] * S[3];
+        S[0] = kmsub(kmul(p[1], S[5]), p[2], S[4]);
+        S[1] = kmsub(kmul(p[2], S[3]), p[0], S[5]);
+        S[2] = kmsub(kmul(p[0], S[4]), p[1], S[3]);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) V[r] += S[r] * v[i];
+        for (int r = 0; r < 6; ++r) V[r] = kmadd(V[r], S[r], v[i]);
         double VS[6];
         mcross(V, S, VS);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) A[r] += VS[r] * v[i];
+        for (int r = 0; r < 6; ++r) A[r] = kmadd(A[r], VS[r], v[i]);
       }
     }
 #pragma unroll

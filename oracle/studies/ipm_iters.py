@@ -21,7 +21,7 @@ from oracle.osqp_ref import OSQPSolverRef, SQPRef, synthetic_batch
 
 
 def ipm_variant(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.01, eta=0.99,
-                zinit="one", eta_rule="const"):
+                zinit="one", eta_rule="const", second_order=True, sigma_pow=3.0):
     """box_ipm.ipm_box with knobs: zinit 'one' (z = 1) or 'mu' (z = mu0 / s, centred start);
     eta_rule 'const' or 'adapt' (eta = max(eta, 1 - mu))."""
     n = len(g)
@@ -62,9 +62,10 @@ def ipm_variant(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.0
         ap = min(box_ipm._ratio(sl, dxa, bm), box_ipm._ratio(su, -dxa, bm))
         ad = min(box_ipm._ratio(zl, dzla, bm), box_ipm._ratio(zu, dzua, bm))
         mua = float(((sl + ap * dxa)[bm] @ (zl + ad * dzla)[bm] + (su - ap * dxa)[bm] @ (zu + ad * dzua)[bm]) / (2 * nb))
-        smu = (mua / mu) ** 3 * mu
-        rl = np.where(bm, sl * zl + dxa * dzla - smu, 0.0)
-        ru = np.where(bm, su * zu - dxa * dzua - smu, 0.0)
+        smu = (mua / mu) ** sigma_pow * mu
+        so = 1.0 if second_order else 0.0
+        rl = np.where(bm, sl * zl + so * dxa * dzla - smu, 0.0)
+        ru = np.where(bm, su * zu - so * dxa * dzua - smu, 0.0)
         ell = g - zl + zu + np.where(bm, rl / sl - ru / su, 0.0) - sig * x
         dx = newton(ell)
         dzl = np.where(bm, (-rl - zl * dx) / sl, 0.0)
@@ -120,6 +121,9 @@ VARIANTS = {
     "theta .1, z = 0.01 / s": {"theta": 0.1, "zinit": "0.01"},
     "theta .2, z = 0.01 / s": {"theta": 0.2, "zinit": "0.01"},
     "theta .2, z = 0.1 / s, eta adapt": {"theta": 0.2, "zinit": "0.1", "eta_rule": "adapt"},
+    "n centred, no second-order term": {"theta": 0.2, "zinit": "0.1", "second_order": False},
+    "n centred, no second-order term, sigma^2": {"theta": 0.2, "zinit": "0.1", "second_order": False, "sigma_pow": 2.0},
+    "n centred, no second-order term, sigma^1": {"theta": 0.2, "zinit": "0.1", "second_order": False, "sigma_pow": 1.0},
     "g theta .15, z = 0.1 / s": {"theta": 0.15, "zinit": "0.1"},
     "g theta .25, z = 0.1 / s": {"theta": 0.25, "zinit": "0.1"},
     "g theta .3, z = 0.1 / s": {"theta": 0.3, "zinit": "0.1"},
