@@ -334,11 +334,11 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
   for (int i = 0; i < 6; ++i) {
     if (i >= j) {
       const double* o = &xs[gg][i][0];
-      cm += o[0];
+      cm = kadd(cm, o[0]);
 #pragma unroll
-      for (int r = 0; r < 3; ++r) { ch[r] += o[1 + r]; chd[r] += o[10 + r]; }
+      for (int r = 0; r < 3; ++r) { ch[r] = kadd(ch[r], o[1 + r]); chd[r] = kadd(chd[r], o[10 + r]); }
 #pragma unroll
-      for (int r = 0; r < 6; ++r) { cI[r] += o[4 + r]; cId[r] += o[13 + r]; }
+      for (int r = 0; r < 6; ++r) { cI[r] = kadd(cI[r], o[4 + r]); cId[r] = kadd(cId[r], o[13 + r]); }
     }
   }
   wave_sync();  // every lane has read round 1
@@ -355,7 +355,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
     if (i >= j) {
       const double* o = &xs[gg][i][0];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) { HC[r] += o[r]; Fc[r] += o[6 + r]; }
+      for (int r = 0; r < 6; ++r) { HC[r] = kadd(HC[r], o[r]); Fc[r] = kadd(Fc[r], o[6 + r]); }
     }
   }
 
@@ -496,7 +496,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
       if (i <= j) {
         const double* Si = &xs[gg][i][12];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) dA[r] += Si[r] * acc[i];
+        for (int r = 0; r < 6; ++r) dA[r] = kmadd(dA[r], Si[r], acc[i]);
       }
     }
   }
@@ -516,7 +516,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
     for (int i = 0; i < 6; ++i) {
       if (i >= j) {
 #pragma unroll
-        for (int r = 0; r < 6; ++r) Fs[r] += xs[gg][i][6 + r];
+        for (int r = 0; r < 6; ++r) Fs[r] = kadd(Fs[r], xs[gg][i][6 + r]);
       }
     }
     double sd[6], t1[6], t2[6];

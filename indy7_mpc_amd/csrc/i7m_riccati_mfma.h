@@ -45,7 +45,8 @@ enum : int {
   MO_KT = 290,   // 78  K~ (6 x 13)
   MO_ZERO = 368,
   MO_ONE = 369,
-  MO_GJ = 370,   // 6 x 40  per-pivot Gauss-Jordan exchange slots
+  MO_GJ = 370,   // 6 x 40  per-pivot Gauss-Jordan exchange slots (diagnostic variant)
+  MO_DUMMY = MO_GJ,  // 64: lane l's sink for the stores it has nothing to write (branch-free)
   MO_TOTAL = 610,
 };
 
@@ -213,6 +214,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   }
 
   constexpr int SE = BOX ? 176 : 140;  // stash length
+  // kbuf tail (K~ 64..77, c_v): 20 doubles; every lane stores one (lane l the entry l % 20)
+  const int l20 = l % 20;
+  const int ko20 = (l20 < 14) ? MO_KT + 64 + l20 : MO_CV + (l20 - 14);
   // stash element e of stage k lives at base(e) + k * stride(e): resolved once per lane for its
   // three elements, so the per-stage loads are one multiply-add each (no divergent selects)
   auto base_of = [&](int e, int& stride) -> const double* {
@@ -267,7 +271,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     if (ABL & 512) tp = tstamp(p0 + p1 + p2);
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
-    if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
+    sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
     wave_sync();
     if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
     double bA[4], bB[2];
@@ -363,13 +367,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       // inside a 16-lane row — so each of the two rows used carries its own copy of H's six
       // columns: row 0 = H 0..5, G~ 0..9; row 1 = H 0..5 again, G~ 10..12 and (HINV) the
       // identity columns, which end as H^-1.  The two copies of H evolve identically.
+      // (stores of lanes with nothing to store go to their own dummy slot: no exec-mask branches)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = lq + 4 * i;
-        if (r < 6) {
-          if (lr < 6) sh[MO_H + 6 * r + lr] = Z11[i];
-          if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
-        }
+        sh[(r < 6 && lr < 6) ? MO_H + 6 * r + lr : MO_DUMMY + l] = Z11[i];
+        sh[(r < 6 && lr < 13) ? MO_G + 13 * r + lr : MO_DUMMY + l] = Z10[i];
       }
       wave_sync();
       double E[6];
@@ -380,9 +383,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       const int cc_own = !(BC & 1) ? l
                          : (l < 16) ? m16 : (l < 32 ? (m16 < 6 ? m16 : (m16 < (HINV ? 15 : 9) ? m16 + 10 : -1)) : -1);
       const int cc = !(BC & 1) ? (l < ncol ? l : ncol - 1) : (cc_own < 0 ? 0 : cc_own);
+      const int eo = (cc < 6) ? MO_H + cc : MO_G + (cc - 6), es = (cc < 6) ? 6 : 13;
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
-        E[i] = (cc < 6) ? sh[MO_H + 6 * i + cc] : (cc < 19 ? sh[MO_G + 13 * i + (cc - 6)] : (i == cc - 19 ? 1.0 : 0.0));
+      for (int i = 0; i < 6; ++i) {
+        E[i] = sh[eo + es * (HINV && cc >= 19 ? 0 : i)];
+        if (HINV && cc >= 19) E[i] = (i == cc - 19) ? 1.0 : 0.0;
+      }
       if (ABL & 512) td = tstamp(E[0] + E[1] + E[2] + E[3] + E[4] + E[5]);
 #pragma unroll
       for (int p = 0; p < 6; ++p) {
@@ -395,9 +401,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
       }
       if (ABL & 512) te = tstamp(E[0] + E[1] + E[2] + E[3] + E[4] + E[5]);
-      if (cc_own >= 6 && cc_own < 19) {  // (BC & 1) == 0: lane l = column l
+      {  // K~ columns (lanes of G~ columns; (BC & 1) == 0: lane l = column l), others to the sink
+        const bool kw = cc_own >= 6 && cc_own < 19;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) sh[MO_KT + 13 * i + (cc_own - 6)] = -E[i];
+        for (int i = 0; i < 6; ++i) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = -E[i];
       }
       if (HINV && cc_own >= 19 && cc_own < 25) {
         double* hk = hinv + ((long)b * (N - 1) + k) * 36;
@@ -423,7 +430,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         }
       }
       kk[l] = sh[MO_KT + l];
-      if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
+      kk[64 + l20] = sh[ko20];  // lanes >= 20 repeat the stores of lanes l % 20 (same values)
     }
   }
 
