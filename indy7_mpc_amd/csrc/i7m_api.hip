@@ -520,6 +520,13 @@ extern "C" {
 
 const char* i7m_last_error(void) { return g_err.c_str(); }
 
+#ifdef I7M_DIAG
+// Diagnostic library only (not declared in include/indy7_mpc.h): point every instrumented
+// kernel of both translation units at a per-wave timeline buffer (i7m_timeline.h; nullptr: off).
+int i7m_lin_tu_set_timeline(void* p);
+int i7m_diag_timeline(void* p) { return (i7m::tl_set(p) == 0 && i7m_lin_tu_set_timeline(p) == 0) ? 0 : -1; }
+#endif
+
 const char* i7m_version(void) { return "indy7_mpc_amd 0.2 (gfx950, fp64, " I7M_BUILD_KIND ") src " I7M_SRC_HASH; }
 
 int i7m_device_count(int* n) {

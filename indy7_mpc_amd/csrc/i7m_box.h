@@ -442,6 +442,7 @@ __device__ __forceinline__ const IpmFusedArgs* kernarg_ipm() {
 template <bool DELTA>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_IPM_WPE, I7M_IPM_WPE)))
 k_ipm_fused(IpmFusedArgs args) {
+  I7M_TL(4);
   const int b = blockIdx.x;
   if (b >= args.P.B) return;
   __shared__ double sh[MO_TOTAL];

@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "i7m_timeline.h"
+
 namespace i7m {
 
 // Workgroup barrier ordering LDS only (an LDS-scoped release / acquire around s_barrier, which

@@ -448,6 +448,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(I7M
                                                    ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
                                                    int iter, int mode, const double* __restrict__ lin = nullptr,
                                                    const double* __restrict__ cost = nullptr) {
+  I7M_TL(3);
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;

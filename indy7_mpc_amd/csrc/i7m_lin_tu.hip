@@ -21,6 +21,11 @@ namespace {
 // events of i7m_api.hip's kernel timing (ea / eb may be null).  model: DevModel*, params:
 // SolveParams*, init_stats: ProblemStats* (i7m_kernels.h).
 // fext_world: fext (non-null) is a world-frame wrench (k_linearize<., true>).
+#ifdef I7M_DIAG
+// this unit's copy of the timeline buffer pointer (i7m_timeline.h; set by i7m_diag_timeline)
+extern "C" int i7m_lin_tu_set_timeline(void* p) { return i7m::tl_set(p); }
+#endif
+
 void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* model,
                                  const void* params, const double* xu, const double* goals, const double* fext,
                                  bool fext_world, const int* active, double* lin, double* cost, double* qpd,

@@ -610,6 +610,7 @@ __global__ void __launch_bounds__(64) I7M_LIN_OCC k_linearize(const DevModel* __
                                                   double* __restrict__ lin, double* __restrict__ cost,
                                                   double* __restrict__ qpd = nullptr, int* __restrict__ init_active = nullptr,
                                                   ProblemStats* __restrict__ init_stats = nullptr) {
+  I7M_TL(1);
   const int l = threadIdx.x;
   const int g = l / 6;
   const int j = l - 6 * g;

@@ -214,6 +214,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   }
 
   constexpr int SE = BOX ? 176 : 140;  // stash length
+  // Branch-free lane-conditional stores (lanes with nothing to store write a per-lane sink slot,
+  // DESIGN.md §7) in the plain QP only: in the box body (k_ipm_fused) the sink addresses and
+  // the duplicated tail stores raised its VGPR spill 35 -> 78 and the launch 6.3 -> 8.4 ms, so
+  // it keeps the exec-masked stores.
+  constexpr bool BF = !BOX;
   // kbuf tail (K~ 64..77, c_v): 20 doubles; every lane stores one (lane l the entry l % 20)
   const int l20 = l % 20;
   const int ko20 = (l20 < 14) ? MO_KT + 64 + l20 : MO_CV + (l20 - 14);
@@ -271,7 +276,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     if (ABL & 512) tp = tstamp(p0 + p1 + p2);
     sh[MO_AQ + l] = p0;
     sh[MO_AQ + l + 64] = p1;
-    sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
+    if (BF) sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
+    else if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
     wave_sync();
     if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
     double bA[4], bB[2];
@@ -371,8 +377,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = lq + 4 * i;
-        sh[(r < 6 && lr < 6) ? MO_H + 6 * r + lr : MO_DUMMY + l] = Z11[i];
-        sh[(r < 6 && lr < 13) ? MO_G + 13 * r + lr : MO_DUMMY + l] = Z10[i];
+        if (BF) {
+          sh[(r < 6 && lr < 6) ? MO_H + 6 * r + lr : MO_DUMMY + l] = Z11[i];
+          sh[(r < 6 && lr < 13) ? MO_G + 13 * r + lr : MO_DUMMY + l] = Z10[i];
+        } else if (r < 6) {
+          if (lr < 6) sh[MO_H + 6 * r + lr] = Z11[i];
+          if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
+        }
       }
       wave_sync();
       double E[6];
@@ -404,7 +415,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       {  // K~ columns (lanes of G~ columns; (BC & 1) == 0: lane l = column l), others to the sink
         const bool kw = cc_own >= 6 && cc_own < 19;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = -E[i];
+        for (int i = 0; i < 6; ++i) {
+          if (BF) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = -E[i];
+          else if (kw) sh[MO_KT + 13 * i + (cc_own - 6)] = -E[i];
+        }
       }
       if (HINV && cc_own >= 19 && cc_own < 25) {
         double* hk = hinv + ((long)b * (N - 1) + k) * 36;
@@ -430,7 +444,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         }
       }
       kk[l] = sh[MO_KT + l];
-      kk[64 + l20] = sh[ko20];  // lanes >= 20 repeat the stores of lanes l % 20 (same values)
+      if (BF) kk[64 + l20] = sh[ko20];  // lanes >= 20 repeat the stores of lanes l % 20 (same values)
+      else if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
     }
   }
 
@@ -691,6 +706,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
                                                      double* __restrict__ kbuf, double* __restrict__ sol,
                                                      const double* __restrict__ bsig = nullptr,
                                                      const double* __restrict__ bh = nullptr) {
+  I7M_TL(2);
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
