@@ -75,6 +75,7 @@ struct Timing {
 // k_riccati_mfma's Gauss-Jordan pivot broadcasts switch from v_readlane to DPP from this batch
 // size on (riccati_mfma_body BC)
 constexpr int RIC_DPP_MIN_B = 2048;
+constexpr int RIC_PRIO_MIN_B = 1024;  // as many problems as SIMDs: Riccati waves start sharing SIMDs
 
 struct i7m_handle {
   i7m_config cfg;
@@ -285,7 +286,10 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
     // cross-lane broadcasts (riccati_mfma_body BC): the rollout's by DPP at every batch size; the
     // pivots' by DPP from RIC_DPP_MIN_B problems on (fewer instructions) and by v_readlane below
     // (shorter chain); I7M_RIC_BC=0..3 forces one (A/B)
-    const int bc = h->ric_bc >= 0 ? h->ric_bc : (P.B >= RIC_DPP_MIN_B ? 3 : 2);
+    // wave priority by progress (BC bit 2) once SIMDs hold more than one wave: -6 % at B = 4096,
+    // -4 % at B = 1024 (uneven dispatch puts two waves on some SIMDs), +1 us at B = 64
+    const int bc = h->ric_bc >= 0 ? h->ric_bc
+                                  : (P.B >= RIC_DPP_MIN_B ? 3 : 2) | (P.B >= RIC_PRIO_MIN_B ? 4 : 0);
     auto go = [&](auto kern) {
       hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
                             sol, (const double*)nullptr, (const double*)nullptr);
@@ -294,6 +298,8 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       case 1: go(k_riccati_mfma<0, false, 1>); break;
       case 2: go(k_riccati_mfma<0, false, 2>); break;
       case 3: go(k_riccati_mfma<0, false, 3>); break;
+      case 6: go(k_riccati_mfma<0, false, 6>); break;
+      case 7: go(k_riccati_mfma<0, false, 7>); break;
       default: go(k_riccati_mfma<0, false, 0>);
     }
 #endif
@@ -613,7 +619,10 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
-  if (const char* e = std::getenv("I7M_RIC_BC")) h->ric_bc = std::atoi(e) & 3;
+  if (const char* e = std::getenv("I7M_RIC_BC")) {
+    const int v = std::atoi(e) & 7;
+    h->ric_bc = (v == 4 || v == 5) ? (v & 3) : v;  // instantiated: 0 1 2 3 6 7
+  }
   h->pipeline = cfg->pipeline;
   if (const char* e = std::getenv("I7M_PIPE"))
     h->pipeline = std::strcmp(e, "fused") == 0 ? I7M_PIPE_FUSED

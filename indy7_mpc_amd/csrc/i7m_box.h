@@ -477,6 +477,8 @@ k_ipm_fused(IpmFusedArgs args) {
     __syncthreads();
     const IpmFusedArgs* B = kernarg_ipm();
     const BoxParams BP = B->BP;
+    // the most work left first: remaining iterations ~ log(mu / tol) (mu_0 = z0 = 0.1, tol 1e-8)
+    if (I7M_PRIO & 4) set_prio((int)(log10(fmax(S.mu / BP.tol, 1.0)) * (1.0 / 2.5)));
     if (half == 0) {
       ipm_pred_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
       ipm_uniform(S);

@@ -39,6 +39,21 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+// Wave priority (s_setprio 0..3; the SIMD's instruction arbiter otherwise favours the oldest
+// wave).  The Riccati recursion sets it by progress (riccati_mfma_body, BC bit 2: equal-work
+// waves, the one furthest behind first).  I7M_PRIO bits: 1 the line-search rounds, later rounds
+// first (measured no change: 78.4 vs 78.8 us at B = 4096, not default), 2 the interior-point
+// iterations of k_ipm_fused, the most work left first (6.00 -> 5.92 ms per QP, default).
+#ifndef I7M_PRIO
+#define I7M_PRIO 4
+#endif
+__device__ __forceinline__ void set_prio(int p) {  // p wave-uniform; s_setprio takes an immediate
+  if (p <= 0) __builtin_amdgcn_s_setprio(0);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(3);
+}
+
 // ... and for global memory too (a lane reads what another lane of the wave stored): the
 // __syncthreads() of a single-wave workgroup, without the barrier.
 __device__ __forceinline__ void wave_sync_all() {

@@ -353,6 +353,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   double base = 0.0;
   int found = zero_step ? 1 : -1;
   for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R * W) {
+    if (I7M_PRIO & 2) set_prio((c0 - cstart) / (R * W));  // later rounds first: the longest searches
     const int cw = c0 + w * R;  // this wave's first candidate of the round
     const int cand = cw + slot;
     double o[4] = {0.0, 0.0, 0.0, 0.0};

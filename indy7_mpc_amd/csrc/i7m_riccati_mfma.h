@@ -133,12 +133,32 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // HINV (box predictor steps): also carry the identity through the elimination and store H^-1
 // of every stage in hinv (B, N-1, 36) for riccati_delta_body (column-per-lane elimination).
 // BC: cross-lane broadcasts by DPP row_newbcast instead of v_readlane — bit 0 the Gauss-Jordan
-// pivot columns, bit 1 the rollout's x and u; bit-identical either way.  Measured (DESIGN.md
+// pivot columns, bit 1 the rollout's x and u; bit-identical either way.  Bit 2: wave priority by
+// progress (ric_prio_back / _fwd), for launches with several waves per SIMD.  Measured (DESIGN.md
 // §4.2): bit 1 helps at every batch size; bit 0 helps at B = 4096 (fewer instructions) and
 // costs ~4.5 us per launch at B <= 256 (a longer pivot chain), so launch_riccati sets it by
 // batch size.  The config-4 body (BOX, k_ipm_fused) takes bit 1 only: with DPP pivots its
 // fused interior-point kernel spills more (10.7 -> 12.2 ms per QP); the DPP rollout alone
 // gives 10.68 -> 10.60 ms.
+#ifndef I7M_RIC_PRIO_S
+#define I7M_RIC_PRIO_S 1  // 0: quarters of the backward sweep (A/B: 113.8 vs 112.8 us at B = 4096)
+#endif
+// Wave priority by progress (BC bit 2, several waves per SIMD): every problem is the same amount
+// of work, and the SIMD's oldest-first arbitration otherwise lets the first wave run ahead while
+// the youngest finishes alone at the end.  Priority falls as a wave advances, so the waves
+// behind are issued first and the four waves of a SIMD finish together.  Backward stage k of
+// N - 1 (k counts down) and forward stage k of the rollout; the default scheme keeps the lowest
+// level short (the second half of the rollout), since the lead a wave takes there is never
+// corrected:
+__device__ __forceinline__ int ric_prio_back(int k, int N) {
+  if (I7M_RIC_PRIO_S == 1) return 2 * k >= N - 1 ? 3 : (4 * k >= N - 1 ? 2 : 1);
+  return (4 * k) / (N - 1);  // 3 .. 0 in quarters of the backward sweep; the rollout at 0
+}
+__device__ __forceinline__ int ric_prio_fwd(int k, int N) {
+  if (I7M_RIC_PRIO_S == 1) return 2 * k < N - 1 ? 1 : 0;
+  return 0;
+}
+
 template <int ABL, bool BOX, bool HINV = false, int BC = 0>
 __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
                                                   const double* __restrict__ xs, const double* __restrict__ lin,
@@ -149,6 +169,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
                                                   double* __restrict__ hinv = nullptr) {
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
+  constexpr bool PRIO = (BC & 4) && !BOX;
   const double dt = P.dt;
   const double* X = xu + (long)b * P.T;
   const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -271,6 +292,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     return (long long)__builtin_amdgcn_s_memtime();
   };
   for (int k = N - 2; k >= 0; --k) {
+    if (PRIO) set_prio(ric_prio_back(k, N));
     wave_sync();
     if (ABL & 512) tm0 = tstamp(V[0]);
     if (ABL & 512) tp = tstamp(p0 + p1 + p2);
@@ -502,6 +524,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
   for (int d = 0; d < FD; ++d) fload(f[d], d < N - 1 ? d : 0);
   auto stage = [&](const int k, double* fk) {
+    if (PRIO && I7M_RIC_PRIO_S != 0) set_prio(ric_prio_fwd(k, N));
     double r[19];
     if (ABL & 128) {
 #pragma unroll

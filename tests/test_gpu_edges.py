@@ -217,11 +217,13 @@ def test_fused_pipelines_equal_split(lib, model, N, B):
 def test_riccati_broadcast_variants_bit_identical(lib, model, N, B, monkeypatch):
     """k_riccati_mfma's cross-lane broadcasts (riccati_mfma_body BC: v_readlane, or DPP
     row_newbcast with H's columns duplicated in a second 16-lane row for the pivots) move the
-    same values: whole solves are bit-identical for every variant (I7M_RIC_BC=0..3); B = 2050
-    also runs the automatic choice (DPP pivots from 2048 problems, DPP rollout always)."""
+    same values: whole solves are bit-identical for every variant (I7M_RIC_BC=0..3), and with the
+    progress-priority bit (6, 7: s_setprio per stage changes only the issue order); B = 2050
+    also runs the automatic choice (DPP pivots from 2048 problems, DPP rollout always, priority
+    above 1024)."""
     xcur, goals, XU = synthetic_batch(B, N, seed=600 + N + B)
     outs = {}
-    for bc in ("0", "1", "2", "3", "auto"):
+    for bc in ("0", "1", "2", "3", "6", "7", "auto"):
         if bc == "auto":
             monkeypatch.delenv("I7M_RIC_BC", raising=False)
         else:
@@ -229,7 +231,7 @@ def test_riccati_broadcast_variants_bit_identical(lib, model, N, B, monkeypatch)
         h = lib.Handle(model, N=N, max_batch=B)
         outs[bc] = h.solve(xcur, goals, XU)
         h.close()
-    for bc in ("1", "2", "3", "auto"):
+    for bc in ("1", "2", "3", "6", "7", "auto"):
         np.testing.assert_array_equal(outs[bc][0], outs["0"][0])
         for key in ("qp_iters", "n_alphas", "alphas", "n_steps", "stepsizes"):
             np.testing.assert_array_equal(outs[bc][1][key], outs["0"][1][key])
