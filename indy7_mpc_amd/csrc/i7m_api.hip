@@ -75,6 +75,7 @@ struct Timing {
 // k_riccati_mfma's Gauss-Jordan pivot broadcasts switch from v_readlane to DPP from this batch
 // size on (riccati_mfma_body BC)
 constexpr int RIC_DPP_MIN_B = 2048;
+constexpr int RIC_W2_MAX_B = 128;     // two-wave Riccati up to this batch size (I7M_RIC_W2 forces): 43.9 -> 42.0 us at B = 1, 44.6 -> 42.7 at 64; slower from 512
 constexpr int RIC_PRIO_MIN_B = 1024;  // as many problems as SIMDs: Riccati waves start sharing SIMDs
 
 struct i7m_handle {
@@ -115,6 +116,7 @@ struct i7m_handle {
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
   int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
   int pipeline = I7M_PIPE_AUTO;  // cfg.pipeline, or I7M_PIPE=split|fused
+  int ric_w2 = -1;               // k_riccati_mfma_w2 (two waves per problem): 1 / 0, -1 = by batch size
   int ric_bc = -1;               // k_riccati_mfma broadcast variant (BC bits), -1 = by batch size
   // timing
   bool timing = false;
@@ -290,6 +292,17 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
     // -4 % at B = 1024 (uneven dispatch puts two waves on some SIMDs), +1 us at B = 64
     const int bc = h->ric_bc >= 0 ? h->ric_bc
                                   : (P.B >= RIC_DPP_MIN_B ? 3 : 2) | (P.B >= RIC_PRIO_MIN_B ? 4 : 0);
+    // small batches: two waves per problem (k_riccati_mfma_w2), the stage's MFMA chains split
+    const bool w2 = h->ric_w2 >= 0 ? h->ric_w2 != 0 : P.B <= RIC_W2_MAX_B;
+    if (w2) {
+      auto go2 = [&](auto kern) {
+        hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(128), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active,
+                              W.kbuf, sol);
+      };
+      if (bc & 1) go2(k_riccati_mfma_w2<3>);
+      else go2(k_riccati_mfma_w2<2>);
+      return;
+    }
     auto go = [&](auto kern) {
       hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
                             sol, (const double*)nullptr, (const double*)nullptr);
@@ -619,6 +632,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
   if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
+  if (const char* e = std::getenv("I7M_RIC_W2")) h->ric_w2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_RIC_BC")) {
     const int v = std::atoi(e) & 7;
     h->ric_bc = (v == 4 || v == 5) ? (v & 3) : v;  // instantiated: 0 1 2 3 6 7

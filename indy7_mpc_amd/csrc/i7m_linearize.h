@@ -102,11 +102,28 @@ __device__ __forceinline__ void chol6_solve_lds(const double* Lm, double b[6]) {
   }
 }
 
+// Padding after each knot's six link slots (doubles).  The lanes of a knot read the same slot
+// (a broadcast) while the knots of a ds_read_b128 lane group read different ones, so the knot
+// stride decides the bank conflicts: unpadded (120 doubles = 240 dwords, 48 mod 64 banks) knots
+// g and g + 4 share banks and every slot read was a 2-way conflict (SQ_LDS_BANK_CONFLICT: 3.3
+// extra cycles per LDS instruction); 124 doubles (56 mod 64) give every knot of each lane group
+// ({0,2,3,4}, {0..5}, {5,7,8,9}, {6,7,8} + the idle lanes, which read knot KPW - 1) its own
+// four banks.
+#ifndef I7M_LIN_XPAD
+#define I7M_LIN_XPAD 4
+#endif
+struct alignas(16) KnotSlots {
+  double s[6][XS];
+#if I7M_LIN_XPAD > 0
+  double pad[I7M_LIN_XPAD];
+#endif
+  __device__ __forceinline__ double* operator[](int i) { return s[i]; }
+};
 // LDS of one wave's linearisation pass (KPW knots): per-link exchange slots, M, RNEA bias.  16-byte
 // aligned: the slot reads are ds_read_b128 (with 8-byte alignment the compiler falls back to
 // ds_read2_b64, twice the LDS cycles: k_linearize 130 -> 203 us measured).
 struct alignas(16) LinLds {
-  double xs[KPW][6][XS];
+  KnotSlots xs[KPW];
   double sM[KPW][36];
   double st0[KPW][6];
 };
@@ -130,7 +147,7 @@ __device__ __forceinline__ void linearize_body(const DevModel* __restrict__ Mg, 
   const int g = l / 6;
   const int j = l - 6 * g;
   const bool dyn = valid && (k < P.N - 1);
-  const int gg = g < KPW ? g : 0;
+  const int gg = g < KPW ? g : KPW - 1;  // the idle lanes 60..63 shadow the last knot (broadcast reads)
   auto& xs = S.xs;
   auto& sM = S.sM;
   auto& st0 = S.st0;

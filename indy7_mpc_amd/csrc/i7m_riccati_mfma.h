@@ -48,6 +48,8 @@ enum : int {
   MO_GJ = 370,   // 6 x 40  per-pivot Gauss-Jordan exchange slots (diagnostic variant)
   MO_DUMMY = MO_GJ,  // 64: lane l's sink for the stores it has nothing to write (branch-free)
   MO_TOTAL = 610,
+  MO_QX = 610,   // 256  two-wave body: Qxx~ of wave 1 in the accumulator layout (64 i + lane)
+  MO_TOTAL_W2 = 866,
 };
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -159,7 +161,138 @@ __device__ __forceinline__ int ric_prio_fwd(int k, int N) {
   return 0;
 }
 
-template <int ABL, bool BOX, bool HINV = false, int BC = 0>
+// The forward rollout of one problem's QP solution (lane l of its wave, `sh` the body's LDS):
+// x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c, from the gains the backward sweep stored
+// in kbuf (K~, c_v) and the dynamics in lin; writes the minimiser to sol.
+template <int ABL, int BC>
+__device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& P, const double* __restrict__ xs,
+                                                const double* __restrict__ LINb, const double* __restrict__ KB,
+                                                double* __restrict__ sol, double* __restrict__ sh, const int l) {
+  const int N = P.N;
+  const double dt = P.dt;
+  constexpr bool PRIO = (BC & 4) != 0;
+  // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
+  // Lane l < 12 holds x_l and lane m < 6 holds u_m; the lanes of DPP row 0 see the full vectors
+  // through row_newbcast (one 64-bit DPP move per value).  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
+  // (3 per lane) two stages ahead into registers and dropped into one LDS slot permuted so that
+  // the 19 values each lane needs are contiguous: lane m < 6 the row m of K~ (13, then zeros),
+  // lane 6 + i c_v[i] and row i of Aq, Av, Bu; lanes >= 12 an all-zero block.  Every lane then
+  // reads its block with the same ds_read_b128 sequence (no divergent gathers).
+  constexpr int FB = 20;  // doubles per lane block
+  wave_sync_all();  // kbuf stores of the backward sweep -> loads below (other lanes of this wave)
+  double* S = sol + (long)b * P.T;
+  // stage element e of stage k lives at base + k * stride (resolved once per lane)
+  auto fbase = [&](int e, int& stride) -> const double* {
+    if (e < KBUF_STRIDE) {
+      stride = (ABL & 8) ? 0 : KBUF_STRIDE;
+      return KB + e;
+    }
+    stride = (ABL & 16) ? 0 : LIN_STRIDE;
+    return LINb + (e - KBUF_STRIDE);
+  };
+  int fs0, fs1, fs2;
+  const double* fb0 = fbase(l, fs0);
+  const double* fb1 = fbase(l + 64, fs1);
+  const double* fb2 = fbase(l + 128, fs2);
+  // slot position of stage element e
+  auto fpos = [](int e) -> int {
+    if (e < 78) return FB * (e / 13) + e % 13;
+    if (e < 84) return FB * (6 + e - 78);
+    const int t = e - 84, blk = t / 36, w = t % 36;
+    return FB * (6 + w / 6) + 1 + 6 * blk + w % 6;
+  };
+  const int w0 = fpos(l), w1 = fpos(l + 64), w2 = fpos(l + 128);
+  double* myb = sh + FB * (l < 12 ? l : 12);
+  // zero the slot once (K~ rows' tails and the spare block stay zero)
+  for (int e = l; e < FB * 13; e += 64) sh[e] = 0.0;
+  // FD prefetch buffers used in turn (the loop is unrolled by FD), each refilled FD stages
+  // ahead right after it is dropped into LDS: no register rotation, whose copies made every
+  // stage wait for the loads it had just issued.
+  constexpr int FD = I7M_RIC_FD;
+  double f[FD][3];
+  auto fload = [&](double* f, int kk) {
+    f[0] = fb0[(long)kk * fs0];
+    f[1] = fb1[(long)kk * fs1];
+    f[2] = fb2[(long)kk * fs2];
+  };
+  double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
+  if (l < 12) S[l] = xreg;
+  // drain x_0 before the prefetch: otherwise the waitcnt pass carries the (lane-conditional)
+  // x_0 load into the loop and every stage waits for the loads it has just issued
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+  for (int d = 0; d < FD; ++d) fload(f[d], d < N - 1 ? d : 0);
+  auto stage = [&](const int k, double* fk) {
+    if (PRIO && I7M_RIC_PRIO_S != 0) set_prio(ric_prio_fwd(k, N));
+    double r[19];
+    if (ABL & 128) {
+#pragma unroll
+      for (int j = 0; j < 19; ++j) r[j] = fk[j % 3] * (j + 1);
+      fload(fk, (k + FD < N - 1) ? k + FD : k);
+    } else {
+    wave_sync();
+    sh[w0] = fk[0];
+    sh[w1] = fk[1];
+    sh[w2] = fk[2];
+    fload(fk, (k + FD < N - 1) ? k + FD : k);
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < 19; ++j) r[j] = myb[j];
+    }
+    // x (lanes 0..11, all in DPP row 0) to every lane of the row
+    double X[12];
+    if (BC & 2) {
+      RowBcast<0, 12>::run(xreg, X);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
+    }
+    // u (lanes 0..5): two partial sums to halve the dependency chain
+    double ua = r[12], ub = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
+    const double ureg = ua + ub;
+    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 6) S[18 * k + 12 + l] = ureg;
+    double U[6];
+    if (BC & 2) {
+      RowBcast<0, 6>::run(ureg, U);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
+    }
+    double va = r[0], vb = 0.0, vc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      va += r[1 + j] * X[j];
+      vb += r[7 + j] * X[6 + j];
+      vc += r[13 + j] * ((ABL & 64) ? X[j] : U[j]);
+    }
+    // q lanes: q + dt v, v_l = x_{6+l} from lane l + 6 (DPP row shift, same 16-lane row)
+    const double vq = row_shl6_f64(xreg);
+    const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
+    xreg = nx;
+    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 12) S[18 * (k + 1) + l] = nx;
+  };
+  // all FD stages unconditional inside the loop (the tail after it): a path that skips a stage
+  // and loops back would make the next stage wait for its own refill
+  int k = 0;
+  for (; k + FD - 1 < N - 1; k += FD) {
+#pragma unroll
+    for (int d = 0; d < FD; ++d) stage(k + d, f[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < FD - 1; ++d)
+    if (k + d < N - 1) stage(k + d, f[d]);
+}
+
+// W2: two waves per problem (a 128-lane workgroup, small batches where most SIMDs are idle): the
+// MFMA chains of a stage are split so that the elimination starts after five MFMAs instead of
+// nine and the Qxx chain runs under it — wave 0: W0 = V A~, G~, the Gauss-Jordan elimination,
+// kbuf, the rollout; wave 1: W1 = V B~, H, then W0 and Qxx = A~' W0 + Q~ (handed over through
+// LDS, MO_QX).  Both waves form V~ <- Qxx + K~' G~ from the same operands (wave 1 reads G~ from
+// the elimination's LDS copy), so they hold bit-identical V~ and the result is bit-identical to
+// the one-wave body.  Three workgroup barriers per stage (stash, H / G~, K~ / Qxx).
+template <int ABL, bool BOX, bool HINV = false, int BC = 0, bool W2 = false>
 __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams& P, const double* __restrict__ xu,
                                                   const double* __restrict__ xs, const double* __restrict__ lin,
                                                   const double* __restrict__ cost, const double* __restrict__ qpd,
@@ -167,9 +300,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
                                                   const double* __restrict__ bsig, const double* __restrict__ bh,
                                                   double* __restrict__ sh, const int l,
                                                   double* __restrict__ hinv = nullptr) {
+  static_assert(!W2 || (!BOX && !HINV && ABL == 0), "two-wave body: plain QP only");
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
-  constexpr bool PRIO = (BC & 4) && !BOX;
+  constexpr bool PRIO = (BC & 4) && !BOX && !W2;
+  const int w = W2 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const double dt = P.dt;
   const double* X = xu + (long)b * P.T;
   const double* LINb = lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -280,7 +415,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[MO_HB + l] = bh[(long)b * P.T + 18 * (N - 1) + l];
     }
   }
-  wave_sync();
+  if (W2) lds_sync(); else wave_sync();
   d4 V;
 #pragma unroll
   for (int i = 0; i < 4; ++i) V[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
@@ -292,6 +427,110 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     return (long long)__builtin_amdgcn_s_memtime();
   };
   for (int k = N - 2; k >= 0; --k) {
+    if constexpr (W2) {
+      lds_sync();  // every wave is done with the previous stage's LDS
+      if (w == 0) {
+        sh[MO_AQ + l] = p0;
+        sh[MO_AQ + l + 64] = p1;
+        sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
+      }
+      lds_sync();
+      if (w == 0 && k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
+      double bA[4], bB[2];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
+      bB[0] = sh[offB[0]];
+      bB[1] = sh[offB[1]];
+      d4 W0, Z00, Z10;
+      if (w == 0) {
+        d4 Ni;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ni[i] = sh[oN[i]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
+        Z10 = mfma(bB[0], W0[1], Ni);
+        Z10 = mfma(bB[1], W0[2], Z10);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = lq + 4 * i;
+          sh[(r < 6 && lr < 13) ? MO_G + 13 * r + lr : MO_DUMMY + l] = Z10[i];
+        }
+      } else {
+        d4 Ri;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ri[i] = sh[oR[i]];
+        d4 W1 = {0.0, 0.0, 0.0, 0.0};
+        W1 = mfma(V[1], bB[0], W1);
+        W1 = mfma(V[2], bB[1], W1);
+        d4 Z11 = mfma(bB[0], W1[1], Ri);
+        Z11 = mfma(bB[1], W1[2], Z11);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = lq + 4 * i;
+          sh[(r < 6 && lr < 6) ? MO_H + 6 * r + lr : MO_DUMMY + l] = Z11[i];
+        }
+      }
+      lds_sync();  // H and G~ in LDS
+      if (w == 0) {
+        // column-per-lane Gauss-Jordan on [H | G~], as in the one-wave body below
+        double E[6];
+        const int m16 = l & 15;
+        const int cc_own = !(BC & 1) ? l : (l < 16) ? m16 : (l < 32 ? (m16 < 6 ? m16 : (m16 < 9 ? m16 + 10 : -1)) : -1);
+        const int cc = !(BC & 1) ? (l < 19 ? l : 18) : (cc_own < 0 ? 0 : cc_own);
+        const int eo = (cc < 6) ? MO_H + cc : MO_G + (cc - 6), es = (cc < 6) ? 6 : 13;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) E[i] = sh[eo + es * i];
+#pragma unroll
+        for (int p = 0; p < 6; ++p) {
+          double Pc[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) Pc[i] = (BC & 1) ? row_bcast_f64_at(E[i], p) : readlane_f64(E[i], p);
+          const double inv = rcp_nr(Pc[p]);
+          const double ep = E[p] * inv;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) E[i] = (i == p) ? ep : E[i] - Pc[i] * ep;
+        }
+        const bool kw = cc_own >= 6 && cc_own < 19;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = -E[i];
+      } else {
+        d4 Qi;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Qi[i] = sh[q1[i]] * sh[q2[i]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
+        Z00 = Qi;
+        if (lq == 0) Z00[3] += W0[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sh[MO_QX + 64 * i + l] = Z00[i];
+      }
+      lds_sync();  // K~ and Qxx in LDS
+      if (w == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Z00[i] = sh[MO_QX + 64 * i + l];
+      } else {
+        // G~ as wave 0's accumulators held it (rows >= 6 and columns >= 13 are exact zeros there)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = lq + 4 * i;
+          Z10[i] = (r < 6 && lr < 13) ? sh[MO_G + 13 * r + lr] : 0.0;
+        }
+      }
+      V = mfma(sh[oK[0]], Z10[0], Z00);
+      V = mfma(sh[oK[1]], Z10[1], V);
+      if (w == 0) {
+        double* kk = KB + (long)k * KBUF_STRIDE;
+        kk[l] = sh[MO_KT + l];
+        kk[64 + l20] = sh[ko20];
+      }
+      continue;
+    }
     if (PRIO) set_prio(ric_prio_back(k, N));
     wave_sync();
     if (ABL & 512) tm0 = tstamp(V[0]);
@@ -471,119 +710,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     }
   }
 
-  // ---- forward rollout: x_0 = xs; u_k = K~ [x_k; 1]; x_{k+1} = A x + B u + c.
-  // Lane l < 12 holds x_l and lane m < 6 holds u_m; the lanes of DPP row 0 see the full vectors
-  // through row_newbcast (one 64-bit DPP move per value).  A stage's data (K~ 78 | c_v 6 | Aq Av Bu 108 = 192 doubles) is loaded coalesced
-  // (3 per lane) two stages ahead into registers and dropped into one LDS slot permuted so that
-  // the 19 values each lane needs are contiguous: lane m < 6 the row m of K~ (13, then zeros),
-  // lane 6 + i c_v[i] and row i of Aq, Av, Bu; lanes >= 12 an all-zero block.  Every lane then
-  // reads its block with the same ds_read_b128 sequence (no divergent gathers).
-  if (ABL & 1) return;
-  constexpr int FB = 20;  // doubles per lane block
-  wave_sync_all();  // kbuf stores of the backward sweep -> loads below (other lanes of this wave)
-  double* S = sol + (long)b * P.T;
-  // stage element e of stage k lives at base + k * stride (resolved once per lane)
-  auto fbase = [&](int e, int& stride) -> const double* {
-    if (e < KBUF_STRIDE) {
-      stride = (ABL & 8) ? 0 : KBUF_STRIDE;
-      return KB + e;
-    }
-    stride = (ABL & 16) ? 0 : LIN_STRIDE;
-    return LINb + (e - KBUF_STRIDE);
-  };
-  int fs0, fs1, fs2;
-  const double* fb0 = fbase(l, fs0);
-  const double* fb1 = fbase(l + 64, fs1);
-  const double* fb2 = fbase(l + 128, fs2);
-  // slot position of stage element e
-  auto fpos = [](int e) -> int {
-    if (e < 78) return FB * (e / 13) + e % 13;
-    if (e < 84) return FB * (6 + e - 78);
-    const int t = e - 84, blk = t / 36, w = t % 36;
-    return FB * (6 + w / 6) + 1 + 6 * blk + w % 6;
-  };
-  const int w0 = fpos(l), w1 = fpos(l + 64), w2 = fpos(l + 128);
-  double* myb = sh + FB * (l < 12 ? l : 12);
-  // zero the slot once (K~ rows' tails and the spare block stay zero)
-  for (int e = l; e < FB * 13; e += 64) sh[e] = 0.0;
-  // FD prefetch buffers used in turn (the loop is unrolled by FD), each refilled FD stages
-  // ahead right after it is dropped into LDS: no register rotation, whose copies made every
-  // stage wait for the loads it had just issued.
-  constexpr int FD = I7M_RIC_FD;
-  double f[FD][3];
-  auto fload = [&](double* f, int kk) {
-    f[0] = fb0[(long)kk * fs0];
-    f[1] = fb1[(long)kk * fs1];
-    f[2] = fb2[(long)kk * fs2];
-  };
-  double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
-  if (l < 12) S[l] = xreg;
-  // drain x_0 before the prefetch: otherwise the waitcnt pass carries the (lane-conditional)
-  // x_0 load into the loop and every stage waits for the loads it has just issued
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#pragma unroll
-  for (int d = 0; d < FD; ++d) fload(f[d], d < N - 1 ? d : 0);
-  auto stage = [&](const int k, double* fk) {
-    if (PRIO && I7M_RIC_PRIO_S != 0) set_prio(ric_prio_fwd(k, N));
-    double r[19];
-    if (ABL & 128) {
-#pragma unroll
-      for (int j = 0; j < 19; ++j) r[j] = fk[j % 3] * (j + 1);
-      fload(fk, (k + FD < N - 1) ? k + FD : k);
-    } else {
-    wave_sync();
-    sh[w0] = fk[0];
-    sh[w1] = fk[1];
-    sh[w2] = fk[2];
-    fload(fk, (k + FD < N - 1) ? k + FD : k);
-    wave_sync();
-#pragma unroll
-    for (int j = 0; j < 19; ++j) r[j] = myb[j];
-    }
-    // x (lanes 0..11, all in DPP row 0) to every lane of the row
-    double X[12];
-    if (BC & 2) {
-      RowBcast<0, 12>::run(xreg, X);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
-    }
-    // u (lanes 0..5): two partial sums to halve the dependency chain
-    double ua = r[12], ub = 0.0;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
-    const double ureg = ua + ub;
-    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 6) S[18 * k + 12 + l] = ureg;
-    double U[6];
-    if (BC & 2) {
-      RowBcast<0, 6>::run(ureg, U);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
-    }
-    double va = r[0], vb = 0.0, vc = 0.0;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      va += r[1 + j] * X[j];
-      vb += r[7 + j] * X[6 + j];
-      vc += r[13 + j] * ((ABL & 64) ? X[j] : U[j]);
-    }
-    // q lanes: q + dt v, v_l = x_{6+l} from lane l + 6 (DPP row shift, same 16-lane row)
-    const double vq = row_shl6_f64(xreg);
-    const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
-    xreg = nx;
-    if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 12) S[18 * (k + 1) + l] = nx;
-  };
-  // all FD stages unconditional inside the loop (the tail after it): a path that skips a stage
-  // and loops back would make the next stage wait for its own refill
-  int k = 0;
-  for (; k + FD - 1 < N - 1; k += FD) {
-#pragma unroll
-    for (int d = 0; d < FD; ++d) stage(k + d, f[d]);
+  if (W2) {
+    lds_sync();  // wave 1's last reads of the stage LDS before the rollout reuses it
+    if (w != 0) return;
   }
-#pragma unroll
-  for (int d = 0; d < FD - 1; ++d)
-    if (k + d < N - 1) stage(k + d, f[d]);
+  if (ABL & 1) return;
+  riccati_rollout<ABL, BC>(b, P, xs, LINb, KB, sol, sh, l);
 }
 
 // The corrector Newton step of I7M_QP_BOX (k_ipm_fused): the QP of the last
@@ -719,6 +851,22 @@ __device__ __forceinline__ void riccati_delta_body(const int b, const SolveParam
     stage(k + 1, fb);
   }
   if (k < N - 1) stage(k, fa);
+}
+
+// Two waves per problem (riccati_mfma_body W2), for small batches.
+template <int BC>
+__global__ void __launch_bounds__(128) k_riccati_mfma_w2(SolveParams P, const double* __restrict__ xu,
+                                                       const double* __restrict__ xs, const double* __restrict__ lin,
+                                                       const double* __restrict__ cost, const double* __restrict__ qpd,
+                                                       const int* __restrict__ active, double* __restrict__ kbuf,
+                                                       double* __restrict__ sol) {
+  I7M_TL(2);
+  const int b = blockIdx.x;
+  if (b >= P.B) return;
+  if (active && !active[b]) return;
+  __shared__ double sh[MO_TOTAL_W2];
+  riccati_mfma_body<0, false, false, BC, true>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, nullptr, nullptr, sh,
+                                               threadIdx.x & 63);
 }
 
 template <int ABL, bool BOX = false, int BC = 0>

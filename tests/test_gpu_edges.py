@@ -239,6 +239,25 @@ def test_riccati_broadcast_variants_bit_identical(lib, model, N, B, monkeypatch)
     _check_sqp(outs["3"][0][idx], outs["3"][1][idx], xcur[idx], goals[idx], XU[idx], N=N)
 
 
+@pytest.mark.parametrize("N,B", [(32, 5), (2, 4), (20, 7), (64, 3), (32, 2050)])
+def test_riccati_two_wave_body_bit_identical(lib, model, N, B, monkeypatch):
+    """k_riccati_mfma_w2 (two waves per problem: W0 / G~ / elimination on wave 0, W1 / H / Qxx on
+    wave 1, V~ formed by both from the same operands) gives bit-identical solves to the one-wave
+    kernel, with either pivot broadcast (B = 2050 takes the DPP pivots)."""
+    xcur, goals, XU = synthetic_batch(B, N, seed=700 + N + B)
+    outs = {}
+    for w2 in ("0", "1"):
+        monkeypatch.setenv("I7M_RIC_W2", w2)
+        h = lib.Handle(model, N=N, max_batch=B)
+        outs[w2] = h.solve(xcur, goals, XU)
+        h.close()
+    np.testing.assert_array_equal(outs["1"][0], outs["0"][0])
+    for key in ("qp_iters", "n_alphas", "alphas", "n_steps", "stepsizes"):
+        np.testing.assert_array_equal(outs["1"][1][key], outs["0"][1][key])
+    idx = [0, B - 1]
+    _check_sqp(outs["1"][0][idx], outs["1"][1][idx], xcur[idx], goals[idx], XU[idx], N=N)
+
+
 @pytest.mark.parametrize("frame", ["local", "world"])
 def test_fused_pipeline_with_wrench(lib, model, frame):
     N, B = 16, 6
