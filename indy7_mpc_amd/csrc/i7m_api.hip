@@ -273,6 +273,7 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
 #ifdef I7M_DIAG
     // I7M_ABLATE -> ABL bits of riccati_mfma_body (diagnostic timing builds, results invalid;
     // compiled only into the -DI7M_DIAG library that tools/ load, never the shipping one)
+    bool ablated = true;
     switch (h->ablate) {
       case 1: launch_riccati_mfma<1>(s, ea, eb, W, P, xu, xs, active, sol); break;      // no rollout
       case 2: launch_riccati_mfma<6>(s, ea, eb, W, P, xu, xs, active, sol); break;      // scaling for GJ
@@ -282,9 +283,12 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       case 13: launch_riccati_mfma<32>(s, ea, eb, W, P, xu, xs, active, sol); break;    // rollout dead
       case 18: launch_riccati_mfma<448>(s, ea, eb, W, P, xu, xs, active, sol); break;   // rollout chain only
       case 19: launch_riccati_mfma<513>(s, ea, eb, W, P, xu, xs, active, sol); break;   // phase timestamps, no rollout
-      default: launch_riccati_mfma<0>(s, ea, eb, W, P, xu, xs, active, sol);
+      default: ablated = false;
     }
-#else
+    if (ablated) return;
+#endif
+    // (the diag library's default path is the release selection below, so its per-wave timelines
+    // show the shipping kernels)
     // cross-lane broadcasts (riccati_mfma_body BC): the rollout's by DPP at every batch size; the
     // pivots' by DPP from RIC_DPP_MIN_B problems on (fewer instructions) and by v_readlane below
     // (shorter chain); I7M_RIC_BC=0..3 forces one (A/B)
@@ -315,7 +319,6 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       case 7: go(k_riccati_mfma<0, false, 7>); break;
       default: go(k_riccati_mfma<0, false, 0>);
     }
-#endif
   });
 }
 
