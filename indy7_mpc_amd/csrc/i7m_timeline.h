@@ -30,8 +30,9 @@ struct TlScope {
       // s_getreg: HW_ID (id 4) and XCC_ID (id 20), all 32 bits
       const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
       const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-      const unsigned long long i = ((unsigned long long)kid << 16) + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-      if (i < tl[1]) {
+      const unsigned long long wv = (unsigned long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      const unsigned long long i = ((unsigned long long)kid << 16) + wv;
+      if (wv < (1ULL << 16) && i < tl[1]) {  // (a launch of more than 65536 waves records its first 65536)
         unsigned long long* r = tl + 8 + 4 * i;
         r[0] = t0;
         r[1] = t1;
