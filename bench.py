@@ -3,9 +3,11 @@
 A "step" = one full SQP_OSQP.sqp solve (<=2 x linearise + QP + line search, src/osqp_sqp.py:76-93)
 of every problem in the per-GPU batch, inputs resident in HBM.  Multi-GPU: one process per GPU
 (torch.distributed.run), each rank solves its own shard (weak scaling, no data-path collective);
-a gloo barrier brackets the timed region and the max time over ranks is reported.
+a gloo barrier brackets the timed region and the max time over ranks is reported.  One GPU runs
+config 3 (B = 4096, seed 45); N ranks run config 5 (one global batch of N x 4096, seed 47, a
+contiguous shard per rank).  `--gpus N` without a launcher starts the N ranks itself.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--N 32]
+    python bench.py [--gpus N [--share-devices]] [--steps K] [--warmup W] [--batch B] [--N 32]
 """
 from __future__ import annotations
 
@@ -257,9 +259,39 @@ def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps
             "instances_alive_at_end": int(np.isfinite(d[-1]).sum()), "finite": bool(np.isfinite(q[np.isfinite(q)]).all())}
 
 
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) run without a torch.distributed launcher: start N ranks as
+    ONE child process, `python -m torch.distributed.run --nproc-per-node N ... bench.py <same
+    args>`, and return its exit status; rank 0 prints the JSON line.  This process never
+    initialises HIP (torch.cuda.device_count() only counts devices on this image), so the ranks
+    are started from a GPU-clean parent.  More ranks than visible devices is refused unless
+    --share-devices asks for a rehearsal on fewer GPUs."""
+    import socket
+    import subprocess
+
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if args.gpus > ndev and not args.share_devices:
+        print(f"bench.py: --gpus {args.gpus} but only {ndev} device(s) visible; pass --share-devices to "
+              f"rehearse {args.gpus} ranks on {ndev} device(s)", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks = GPUs; without WORLD_SIZE in the environment "
+                                                        "bench.py starts them itself (torch.distributed.run)")
+    ap.add_argument("--share-devices", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices round-robin: a rehearsal of the "
+                         "multi-rank path on a small box, reported as such)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
@@ -272,10 +304,16 @@ def main():
     ap.add_argument("--config4-steps", type=int, default=3)
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (B=64) extra object")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     # the CPU port for this host is compiled (a child process) before anything touches the GPU
     native = build_native_port() if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
     import torch
@@ -294,16 +332,21 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
-    # one rank per GPU (LOCAL_RANK); with fewer visible GPUs than ranks (a rehearsal of the
-    # multi-rank path on a small box) ranks share devices round-robin
+    # one rank per GPU (LOCAL_RANK); more ranks than visible GPUs only as an explicit rehearsal
+    # (--share-devices: ranks share devices round-robin, and the line says how many were used)
     ndev = torch.cuda.device_count()
-    local = local % ndev if ndev > 0 else local
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if world > ndev and not args.share_devices:
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} visible device(s); --share-devices rehearses that")
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.model import default_model
-    from indy7_mpc_amd.synthetic import make_batch
+    from indy7_mpc_amd.sharding import shard_range
+    from indy7_mpc_amd.synthetic import draw_states
 
     B, N = args.batch, args.N
     T = 18 * N - 6
@@ -313,8 +356,16 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     h.set_stream(stream.cuda_stream)
-    seed = 42 + 3 + 1000 * rank  # config 3 (seed = 42 + config index), per-rank shard
-    xcur, goals, XU = make_batch(h, model, B, N, seed)
+    # SURVEY.md §8d seeds = 42 + config index: one GPU runs config 3 (B = 4096, seed 45); N ranks
+    # run config 5 (a global batch of N x B problems drawn with seed 47, rank r solving its
+    # contiguous shard sharding.shard_range(N B, r, N): 8 x 4096 = B 32768 at N = 8)
+    seed = 45 if world == 1 else 47
+    lo, hi = shard_range(B * world, rank, world)
+    xs_all, qg_all = draw_states(model, B * world, seed)
+    xcur, qg = xs_all[lo:hi], qg_all[lo:hi]
+    goals = np.tile(h.eepos(qg), (1, N))
+    XU = np.zeros((B, T))
+    XU[:, :12] = xcur
     t_xu = torch.from_numpy(XU).to(dev)
     t_xs = torch.from_numpy(xcur).to(dev)
     t_goal = torch.from_numpy(goals).to(dev)
@@ -388,6 +439,13 @@ def main():
         if i >= 3:
             h2h.append(time.perf_counter() - a)
 
+    # the devices the ranks actually ran on (a --share-devices rehearsal puts several on one)
+    devs = [local]
+    if world > 1:
+        parts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, torch.tensor([local], dtype=torch.int64))
+        devs = [int(p.item()) for p in parts]
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -424,9 +482,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (random start/goal states, SURVEY.md §8d, seed 45+1000*rank)",
-        "config": {"workload": f"config3: B={B} problems/GPU, N={N}, full SQP (<=2 QP + line search), exact KKT",
+        "data": (f"synthetic (random start/goal states, SURVEY.md §8d, seed {seed}"
+                 + (f": one global batch of {B * world}, contiguous shard per rank)" if world > 1 else ")")),
+        "config": {"workload": (f"config3: B={B} problems/GPU, N={N}" if world == 1 else
+                                f"config5: B={B * world} = {world} x {B} problems, N={N}, sharded one shard per rank")
+                               + ", full SQP (<=2 QP + line search), exact KKT",
                    "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)",
+                   "devices_used": sorted(set(devs)), "shared_devices": len(set(devs)) < world,
                    "value_definition": "device-resident: inputs already in HBM, B*world*steps / (max over ranks of "
                                        "the barrier-to-barrier wall time of K back-to-back solves); BASELINE.md 4's "
                                        "host-to-host rate (H2D + solve + D2H, median) is host_to_host_solves_per_s"},

@@ -68,6 +68,12 @@ extern "C" {
 #define I7M_MAX_SQP 8
 #define I7M_MAX_N 64
 
+/* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature or struct
+ * layout changes.  2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and
+ * i7m_set_external_wrench a trailing `frame` (0.2 builds); 1 had neither.  A caller built against
+ * another revision must not call through this library: compare first. */
+#define I7M_ABI_VERSION 2
+
 #define I7M_OK 0
 #define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */
 #define I7M_EHIP -2     /* HIP runtime error */
@@ -77,8 +83,9 @@ extern "C" {
 enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1 };
 /* How a solve is launched (I7M_QP_DIRECT): FUSED = one kernel per solve (a workgroup per
  * problem runs every SQP iteration's linearisation, QP and line search), FUSED_ITER = that kernel
- * once per SQP iteration, SPLIT = three kernels per SQP iteration; AUTO picks by batch size
- * (DESIGN.md §4.5).  Bit-identical results in every mode. */
+ * once per SQP iteration, SPLIT = three kernels per SQP iteration; AUTO = SPLIT at every batch
+ * size (the fused kernel measured slower at every size).  Bit-identical results
+ * in every mode. */
 enum { I7M_PIPE_AUTO = 0, I7M_PIPE_SPLIT = 1, I7M_PIPE_FUSED = 2, I7M_PIPE_FUSED_ITER = 3 };
 #define I7M_BOX_Q 1     /* q_lower <= q <= q_upper    description/indy7.urdf:203-238 <limit> */
 #define I7M_BOX_V 2     /* |v| <= velocity limit */
@@ -133,6 +140,7 @@ typedef struct i7m_handle i7m_handle;
 
 const char* i7m_last_error(void);
 const char* i7m_version(void);
+int i7m_abi_version(void);                        /* == I7M_ABI_VERSION of the header it was built with */
 int i7m_config_default(i7m_config* cfg);          /* fills everything but `model` */
 int i7m_device_count(int* n);
 
@@ -218,7 +226,8 @@ int i7m_rk4(i7m_handle* h, int32_t Bq, const double* q, const double* v, const d
  * batch-axis analogue of src/gato_mpc_batch.py:76-217.  xstart (B, 12), endpoints (E, 3);
  * dist_out (num_steps, B) goal distances (NaN once an instance has stopped); q_out
  * (num_steps, B, 6) q after each step's plant, xcur_out (B, 12), xu_out (B, T) the final state
- * and warm start: each may be NULL but dist_out.  Synchronous. */
+ * and warm start: each may be NULL but dist_out.  Synchronous.  I7M_EINVAL if the handle has an
+ * external wrench set (MPC_OSQP's loop has none, src/osqp_mpc.py:56). */
 int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* endpoints, int32_t n_endpoints,
                 int32_t num_steps, double* dist_out, double* q_out, double* xcur_out, double* xu_out);
 

@@ -20,6 +20,7 @@ import numpy as np
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
+ABI_VERSION = 2  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8
 MAX_N = 64
@@ -104,6 +105,7 @@ _H = C.c_void_p
 SIGNATURES = [
     ("i7m_last_error", C.c_char_p, []),
     ("i7m_version", C.c_char_p, []),
+    ("i7m_abi_version", C.c_int, []),
     ("i7m_config_default", C.c_int, [C.POINTER(i7m_config)]),
     ("i7m_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("i7m_create", C.c_int, [C.POINTER(i7m_config), C.POINTER(_H)]),
@@ -151,6 +153,8 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.i7m_abi_version() != ABI_VERSION:
+            raise I7MError(f"{path} has C-ABI revision {lib.i7m_abi_version()}, this binding expects {ABI_VERSION}")
         _lib = lib
         return lib
 

@@ -46,6 +46,7 @@ hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipSt
                                 const void* model, const void* params, const double* xu_in, double* xu_out,
                                 const double* xs, const double* goals, const double* fext, double* lin, double* cost,
                                 double* qpd, double* kbuf, double* sol, int* active, void* stats);
+hipError_t i7m_prepare_sqp_fused();
 
 static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
 
@@ -422,14 +423,12 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
 }
 
 // Does this solve run as one k_sqp_fused launch?  (Direct QP only; the box mode's interior point
-// has its own fused kernel between the Riccati and the line search.)  AUTO picks by batch size:
-// DESIGN.md §4.5 has the measurements behind the threshold.
-constexpr int FUSED_AUTO_MAX_B = 0;
+// has its own fused kernel between the Riccati and the line search.)  AUTO is the split pipeline
+// at every batch size: the fused one measured 1.1-2.4x slower from B = 1 to 4096.
 bool use_fused(const i7m_handle* h, int B) {
+  (void)B;
   if (h->cfg.qp_mode != I7M_QP_DIRECT) return false;
-  if (h->pipeline == I7M_PIPE_FUSED || h->pipeline == I7M_PIPE_FUSED_ITER) return true;
-  if (h->pipeline == I7M_PIPE_SPLIT) return false;
-  return B <= FUSED_AUTO_MAX_B;
+  return h->pipeline == I7M_PIPE_FUSED || h->pipeline == I7M_PIPE_FUSED_ITER;
 }
 
 
@@ -549,7 +548,9 @@ int i7m_lin_tu_set_timeline(void* p);
 int i7m_diag_timeline(void* p) { return (i7m::tl_set(p) == 0 && i7m_lin_tu_set_timeline(p) == 0) ? 0 : -1; }
 #endif
 
-const char* i7m_version(void) { return "indy7_mpc_amd 0.2 (gfx950, fp64, " I7M_BUILD_KIND ") src " I7M_SRC_HASH; }
+int i7m_abi_version(void) { return I7M_ABI_VERSION; }
+
+const char* i7m_version(void) { return "indy7_mpc_amd 0.3 (gfx950, fp64, " I7M_BUILD_KIND ") src " I7M_SRC_HASH; }
 
 int i7m_device_count(int* n) {
   if (!n) return fail(I7M_EINVAL, "null");
@@ -646,6 +647,10 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
                    : std::strcmp(e, "fused_iter") == 0 ? I7M_PIPE_FUSED_ITER
                    : std::strcmp(e, "split") == 0 ? I7M_PIPE_SPLIT
                    : h->pipeline;
+  if (h->pipeline == I7M_PIPE_FUSED || h->pipeline == I7M_PIPE_FUSED_ITER) {
+    const hipError_t ef = i7m_prepare_sqp_fused();
+    if (ef != hipSuccess) return bail(fail(I7M_EHIP, std::string("k_sqp_fused LDS limit: ") + hipGetErrorString(ef)));
+  }
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;
   // scratch for the query hooks: >= 114 doubles for each of >= 256 queries
   const size_t scratch = std::max(Bm * T, (size_t)256 * 114);
@@ -980,6 +985,11 @@ int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* en
   if (rc) return rc;
   if (n_endpoints < 1 || num_steps < 0 || !endpoints || !xstart || !dist_out)
     return fail(I7M_EINVAL, "mpc_run: need xstart, >= 1 endpoint, num_steps >= 0, dist_out");
+  // MPC_OSQP has no external wrench (src/osqp_mpc.py:56 calls rk4 without f_ext): with one set
+  // on the handle the planner (run_sqp) would use it and the plant (k_mpc_advance) would not
+  if (h->has_fext)
+    return fail(I7M_EINVAL, "mpc_run: the handle has an external wrench set; MPC_OSQP's closed loop has none "
+                            "(clear it with i7m_set_external_wrench(h, 0, NULL, 0))");
   if (B == 0) return I7M_OK;
   HIPCHK(hipSetDevice(h->dev));
   const int N = h->cfg.N;

@@ -4,7 +4,10 @@
 #include <hip/hip_ext.h>
 
 #include <cmath>
+#include <mutex>
 #include <type_traits>
+
+#include "../../include/indy7_mpc.h"
 
 namespace {
 #include "i7m_fused.h"
@@ -24,10 +27,8 @@ hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipSt
   const size_t lds = fused_lds_bytes(P.T, W);
   const bool fw = fext && fext_world;
   const int it0 = it < 0 ? 0 : it;
+  // the dynamic-LDS limits were raised once, by i7m_prepare_sqp_fused (never inside a capture)
   auto go = [&](auto kern, int threads) -> hipError_t {
-    // dynamic LDS beyond the 64 KB default (4 waves: four linearisation regions)
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
     hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(threads), lds, s, ea, eb, 0, M, P, xu_in, xu_out, xs, goals, fext, lin, cost,
                           qpd, kbuf, sol, active, st, it0);
     return hipGetLastError();
@@ -45,4 +46,38 @@ hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipSt
   using W4 = std::integral_constant<int, 4>;
   if (W == 4) return spec ? pick(T_{}, W4{}) : pick(F_{}, W4{});
   return spec ? pick(T_{}, W1{}) : pick(F_{}, W1{});
+}
+
+// Raise every k_sqp_fused instantiation's dynamic-LDS limit beyond the 64 KB default (four waves
+// hold four linearisation regions) to what the largest horizon needs, once per process; called
+// by i7m_create for a handle that may run the fused pipeline, so launches (and graph captures)
+// never call hipFuncSetAttribute.
+hipError_t i7m_prepare_sqp_fused() {
+  using namespace i7m;
+  static std::once_flag once;
+  static hipError_t err = hipSuccess;
+  std::call_once(once, [] {
+    auto set = [](auto kern, int W) {
+      const int lds = (int)fused_lds_bytes(18 * I7M_MAX_N - 6, W);
+      const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess && err == hipSuccess) err = e;
+    };
+    set(k_sqp_fused<true, 1, false, false>, 1);
+    set(k_sqp_fused<true, 1, false, true>, 1);
+    set(k_sqp_fused<true, 1, true, false>, 1);
+    set(k_sqp_fused<true, 1, true, true>, 1);
+    set(k_sqp_fused<false, 1, false, false>, 1);
+    set(k_sqp_fused<false, 1, false, true>, 1);
+    set(k_sqp_fused<false, 1, true, false>, 1);
+    set(k_sqp_fused<false, 1, true, true>, 1);
+    set(k_sqp_fused<true, 4, false, false>, 4);
+    set(k_sqp_fused<true, 4, false, true>, 4);
+    set(k_sqp_fused<true, 4, true, false>, 4);
+    set(k_sqp_fused<true, 4, true, true>, 4);
+    set(k_sqp_fused<false, 4, false, false>, 4);
+    set(k_sqp_fused<false, 4, false, true>, 4);
+    set(k_sqp_fused<false, 4, true, false>, 4);
+    set(k_sqp_fused<false, 4, true, true>, 4);
+  });
+  return err;
 }

@@ -5,9 +5,12 @@ Same constructor, attributes and methods.  The numbers come from the GPU:
     with the block-tridiagonal Riccati kernel (k_riccati).  The reference hands the same
     P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.
   * ``Pdata/Adata/l/g`` (the CSC value arrays the reference fills, :95-135) are assembled on
-    the host from the device linearisation, in the reference's exact value order, only when
-    ``update_constraint_matrix`` / ``update_cost_matrix`` are called (they are not needed by
-    the solve itself).
+    the host from the device linearisation, in the reference's exact value order.  The solve
+    itself does not need them, so after ``setup_and_solve_qp`` they are filled lazily: the call
+    records its linearisation point and the first read of any of the four arrays assembles them
+    (one device linearisation of that point, bit-identical to the solve's), as the reference
+    leaves them filled as a side effect of :137-143.  ``update_constraint_matrix`` /
+    ``update_cost_matrix`` fill them at once, like the reference's.
   * ``eepos`` / ``d_eepos`` are device FK / Jacobian queries.
 Extra (not in the reference): ``max_batch`` / ``device_id`` kwargs size the device buffers
 for the batched entry point ``SQP_OSQP.sqp_batch``.
@@ -52,11 +55,12 @@ class OSQPSolver:
         self.regularize = regularize
         self.eps = eps
         self.A = self.initialize_A()
-        self.l = np.zeros(self.N * self.nx)
         self.P = self.initialize_P()
-        self.g = np.zeros(self.traj_len)
-        self.Pdata = np.zeros(self.P.nnz)
-        self.Adata = np.zeros(self.A.nnz)
+        self._l = np.zeros(self.N * self.nx)
+        self._g = np.zeros(self.traj_len)
+        self._Pdata = np.zeros(self.P.nnz)
+        self._Adata = np.zeros(self.A.nnz)
+        self._pending_A = self._pending_P = None  # linearisation point of the last setup_and_solve_qp
         self.A_k = np.vstack([-1.0 * np.eye(self.nx),
                               np.vstack([np.hstack([np.eye(self.nq), self.dt * np.eye(self.nq)]),
                                          np.ones((self.nq, 2 * self.nq))])])
@@ -99,15 +103,75 @@ class OSQPSolver:
 
     def update_constraint_matrix(self, xu, xs, _lin=None):
         lin = self._linearisation(xu, np.zeros(3 * self.N))[0] if _lin is None else _lin
-        self.Adata[:], self.l[:] = assemble_A(lin, np.asarray(xu, float), np.asarray(xs, float), self.dt, self.N)
+        self._pending_A = None
+        self._Adata[:], self._l[:] = assemble_A(lin, np.asarray(xu, float), np.asarray(xs, float), self.dt, self.N)
 
     def update_cost_matrix(self, XU, eepos_g, _cost=None):
         cost = self._linearisation(XU, eepos_g)[1] if _cost is None else _cost
-        self.Pdata[:], self.g[:] = assemble_P(cost, np.asarray(XU, float), self.N)
+        self._pending_P = None
+        self._Pdata[:], self._g[:] = assemble_P(cost, np.asarray(XU, float), self.N)
 
     def setup_and_solve_qp(self, xu, xs, eepos_g):
-        """reference :137-143 — linearise at xu, solve the QP; returns an object with ``.x``."""
-        return QPSolution(self.handle.qp(xu, xs, eepos_g)[0])
+        """reference :137-143 — linearise at xu, solve the QP; returns an object with ``.x``.
+        Pdata / Adata / l / g describe this QP afterwards (assembled on first read)."""
+        xu, xs, eepos_g = (np.array(a, dtype=float) for a in (xu, xs, eepos_g))
+        sol = QPSolution(self.handle.qp(xu, xs, eepos_g)[0])
+        self._pending_A = (xu, xs)
+        self._pending_P = (xu, eepos_g)
+        return sol
+
+    def _flush(self):
+        """Assemble the arrays of the last setup_and_solve_qp that have not been read yet."""
+        pa, pp = self._pending_A, self._pending_P
+        if pa is None and pp is None:
+            return
+        xu = (pa or pp)[0]
+        goals = pp[1] if pp is not None else np.zeros(3 * self.N)
+        lin, cost = self._linearisation(xu, goals)
+        if pa is not None:
+            self.update_constraint_matrix(xu, pa[1], _lin=lin)
+        if pp is not None:
+            self.update_cost_matrix(xu, goals, _cost=cost)
+
+    @property
+    def Pdata(self):
+        self._flush()
+        return self._Pdata
+
+    @Pdata.setter
+    def Pdata(self, value):
+        self._flush()
+        self._Pdata = np.asarray(value, dtype=float)
+
+    @property
+    def Adata(self):
+        self._flush()
+        return self._Adata
+
+    @Adata.setter
+    def Adata(self, value):
+        self._flush()
+        self._Adata = np.asarray(value, dtype=float)
+
+    @property
+    def l(self):  # noqa: E743 - the reference's attribute name
+        self._flush()
+        return self._l
+
+    @l.setter
+    def l(self, value):
+        self._flush()
+        self._l = np.asarray(value, dtype=float)
+
+    @property
+    def g(self):
+        self._flush()
+        return self._g
+
+    @g.setter
+    def g(self, value):
+        self._flush()
+        self._g = np.asarray(value, dtype=float)
 
     def assemble(self, xu, xs, eepos_g):
         """Fill Pdata/Adata/l/g exactly as the reference's update_* methods do."""

@@ -104,3 +104,13 @@ def test_version_is_stamped_with_the_source_tree(lib):
     v = _lib.version()
     assert v.endswith("src " + ge.src_hash()), (v, ge.src_hash())
     assert "release" in v
+
+
+def test_abi_version_matches_header_and_binding(lib, tmp_path):
+    """i7m_abi_version() == the header's I7M_ABI_VERSION == the revision the ctypes binding
+    follows (i7m_aba / i7m_rk4 / i7m_set_external_wrench changed signature under the
+    same names in 0.2, so a caller can only tell the revisions apart by asking)."""
+    from indy7_mpc_amd import _lib
+
+    m = re.search(r"#define\s+I7M_ABI_VERSION\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == lib.i7m_abi_version() == _lib.ABI_VERSION

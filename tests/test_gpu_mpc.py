@@ -82,13 +82,13 @@ def test_notebook_500_step_trace_qualitative(lib, model):
     """The notebook's whole closed-loop run (pin_mpc_indy7.ipynb:98-597, 500 printed goal
     distances) on the device (i7m_mpc_run, B = 1).  The reference solved each QP with OSQP at
     eps 1e-3 and this solver solves it exactly, so the chaotic closed loop drifts: the first 8
-    steps match to 2e-6 (test_mpc_osqp_closed_loop_matches_notebook), the rest qualitatively:
-    no goal switch and no break in 500 steps in either, the same peak step, distances within
-    0.075 everywhere and 0.01 over the last 100 steps, the same settling value to 10 %.
-    Rounding-level changes of the kernels move the trajectory: the largest gap (steps 100-200)
-    measured 0.026, then 0.036, then 0.050 over successive builds, and two builds whose config-3
-    solves agree to 5e-13 relative differ by 0.014 in this trace from step 3 on
-    (tools/lib_diff.py); the last-100 gap stayed within 0.0033-0.0051."""
+    steps match to 2e-6 (test_mpc_osqp_closed_loop_matches_notebook), the rest only
+    qualitatively: no goal switch and no break in 500 steps in either, the same peak step, 0.01
+    over the last 100 steps, the same settling value to 10 %.  There is deliberately no bound on
+    the largest gap mid-run: it moves with every rounding-level change of the kernels (0.026,
+    0.036, 0.050 over successive builds; two builds whose config-3 solves agree to 5e-13 differ by
+    0.014 from step 3 on), so it cannot tell a regression from rounding.  Every step of the loop
+    is pinned instead by test_closed_loop_500_steps_shadowed_by_oracle."""
     tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
     h = lib.Handle(model, N=32, max_batch=1)
     ends = h.eepos(np.array(tr["endpoint_q"]))
@@ -98,6 +98,78 @@ def test_notebook_500_step_trace_qualitative(lib, model):
     assert np.isfinite(d).all()                       # no break (> 1.1)
     assert (d >= 0.1).all() and (ref >= 0.1).all()    # no goal switch (< 0.1)
     assert int(np.argmax(d)) == int(np.argmax(ref))
-    assert np.abs(d - ref).max() < 0.075
     assert np.abs(d[-100:] - ref[-100:]).max() < 1e-2
     assert abs(d[-1] - ref[-1]) < 0.1 * ref[-1]
+
+
+def test_closed_loop_500_steps_shadowed_by_oracle(lib, model):
+    """Shadowing check of the notebook's 500-step closed loop (pin_mpc_indy7.ipynb:98-597,
+    src/osqp_mpc.py:29-70) through the drop-in MPC_OSQP (GPU SQP + GPU rk4 plant): at EVERY
+    step the oracle restarts from the GPU's own state, so no chaotic accumulation enters.
+      * SQP: the C++ port (oracle/cpp/i7m_cpu.cpp, pinned to the numpy oracle by
+        tests/test_oracle.py) solves all 501 recorded (xcur, goal, XU) inputs; the next XU must
+        agree to 1e-9 relative and the alpha sequence and SQP iteration count exactly; every
+        25th step is also solved by the numpy oracle SQPRef (1e-6 relative, alphas exact).
+      * plant: rbd.rk4 from the GPU's state and control must give the GPU's next state to
+        1e-12 relative."""
+    from indy7_mpc_amd.osqp_mpc import MPC_OSQP
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+    from oracle import cpu
+
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    solver = OSQPSolver(model)
+    sqp = SQP_OSQP(solver)
+    rec = []
+    inner = sqp.sqp
+
+    def recording_sqp(xcur, goals, XU):
+        x_in, g_in, xu_in = (np.array(a, dtype=float) for a in (xcur, goals, XU))
+        n0 = len(sqp.stats["linesearch_alphas"]["values"])
+        out = inner(xcur, goals, XU)
+        rec.append((x_in, g_in, xu_in, np.array(out), list(sqp.stats["linesearch_alphas"]["values"][n0:]),
+                    sqp.stats["qp_iters"]["values"][-1]))
+        return out
+
+    sqp.sqp = recording_sqp
+    ctrl = MPC_OSQP(model, sqp, solver)
+    ends = np.array([solver.eepos(np.array(q)) for q in tr["endpoint_q"]])
+    ctrl.run_mpc(np.array(tr["xstart"]), ends, num_steps=500, verbose=False)
+    assert len(rec) == 501 and len(ctrl.xpath) == 500
+
+    xs = np.stack([r[0] for r in rec])
+    gs = np.stack([r[1] for r in rec])
+    xus = np.stack([r[2] for r in rec])
+    outs = np.stack([r[3] for r in rec])
+    ref, qp, al, _ = cpu.solve(xs, gs, xus, 32, nthreads=min(16, os.cpu_count() or 1))
+    rel = np.linalg.norm(outs - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert rel.max() < 1e-9, (int(rel.argmax()), rel.max())
+    for i, r in enumerate(rec):
+        assert r[5] == qp[i], i
+        np.testing.assert_array_equal(np.array(r[4]), al[i][~np.isnan(al[i])], err_msg=f"step {i}")
+    for i in range(0, 501, 25):
+        o = SQPRef(OSQPSolverRef(N=32)).sqp(xs[i], gs[i], xus[i].copy())
+        assert np.linalg.norm(outs[i] - o) / np.linalg.norm(o) < 1e-6, i
+    # plant: MPC step i (record i + 1) drives xcur_i with the first control of the warm start
+    # XU_i it solved from (src/osqp_mpc.py:56); the result is the next record's xcur
+    for i in range(500):
+        x, u = xs[i + 1], xus[i + 1][12:18]
+        qn, vn = rbd.rk4(x[:6], x[6:], u, 0.01)
+        nxt = np.concatenate([qn, vn])
+        got = xs[i + 2] if i < 499 else np.concatenate([ctrl.xpath[-1], np.full(6, np.nan)])
+        k = 12 if i < 499 else 6
+        assert np.linalg.norm(nxt[:k] - got[:k]) <= 1e-12 * np.linalg.norm(nxt[:k]), i
+
+
+def test_mpc_run_refuses_a_handle_with_a_wrench(lib, model):
+    """MPC_OSQP's loop has no external wrench (src/osqp_mpc.py:56): with one set, the planner
+    would use it and the plant would not, so i7m_mpc_run refuses; cleared, it runs."""
+    h = lib.Handle(model, N=16, max_batch=2)
+    ends = np.array([rbd.eepos(np.full(6, 0.3))])
+    xs = np.tile(np.ones(12), (2, 1))
+    h.set_external_wrench(np.ones((2, 6)), frame="world")
+    with pytest.raises(lib.I7MError, match="external wrench"):
+        h.mpc_run(xs, ends, 2)
+    h.set_external_wrench(None)
+    d, _, _, _ = h.mpc_run(xs, ends, 2)
+    assert np.isfinite(d).all()

@@ -51,6 +51,29 @@ def test_golden_linearisation_and_qp(lib, model, N):
         np.testing.assert_array_equal(sol[b][:12], f["xcur"][b])  # x_0 = xs exactly
 
 
+@pytest.mark.parametrize("N", [16, 32])
+def test_setup_and_solve_qp_fills_csc_arrays(lib, model, N):
+    """src/osqp_solver.py:137-143 leaves Pdata / Adata / l / g describing the QP it solved; the
+    drop-in fills them on first read after setup_and_solve_qp (golden fixture values, 1e-10 of
+    max), and a later solve at another point replaces them."""
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+
+    f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
+    s = OSQPSolver(model, N=N)
+    for b in range(f["Pdata"].shape[0]):
+        sol = s.setup_and_solve_qp(f["XU_lin"][b], f["xcur"][b], f["goals"][b]).x
+        assert _rel(sol, f["qp_sol"][b]) < 1e-8
+        for name in ("Pdata", "Adata", "l", "g"):
+            got, ref = getattr(s, name), f[name][b]
+            assert got.shape == ref.shape
+            assert np.abs(got - ref).max() <= 1e-10 * np.abs(ref).max(), (b, name)
+    # an explicit update_* after a solve wins over the pending assembly, like the reference's
+    s.setup_and_solve_qp(f["XU_lin"][0], f["xcur"][0], f["goals"][0])
+    s.update_constraint_matrix(f["XU_lin"][1], f["xcur"][1])
+    assert np.abs(s.Adata - f["Adata"][1]).max() <= 1e-10 * np.abs(f["Adata"][1]).max()
+    assert np.abs(s.Pdata - f["Pdata"][0]).max() <= 1e-10 * np.abs(f["Pdata"][0]).max()
+
+
 @pytest.mark.parametrize("N", [16, 32, 64])
 def test_golden_full_sqp(lib, model, N):
     f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
@@ -168,17 +191,18 @@ def test_bench_scale_properties(lib, model):
         assert _rel(out[b], ref) < 1e-6
 
 
-@pytest.mark.parametrize("N", [32, 64])
-def test_bench_scale_every_problem_matches_cpu_port(lib, model, N):
-    """Config 3 (B = 4096, N = 32) and its N = 64 sibling in full: every problem against the C++
+@pytest.mark.parametrize("B,N,seed", [(4096, 32, 77), (4096, 64, 109), (64, 32, 44)])
+def test_bench_scale_every_problem_matches_cpu_port(lib, model, B, N, seed):
+    """Config 3 (B = 4096, N = 32), its N = 64 sibling and config 2 at its own size (B = 64,
+    N = 32, seed 44 = 42 + config index) in full: every problem against the C++
     restatement (oracle/cpp/i7m_cpu.cpp, same SQP and exact KKT solve, itself pinned to the numpy
-    oracle by tests/test_oracle.py): alpha sequences and SQP iteration counts identical for all
-    4096 problems, XU within 1e-9 relative (SURVEY.md 8d's gate is 1e-4).  At B >= 2048 the
-    Riccati kernel runs its DPP-pivot variant, so this is that variant's full-size check."""
+    oracle by tests/test_oracle.py): alpha sequences and SQP iteration counts identical for every
+    problem, XU within 1e-9 relative (SURVEY.md 8d's gate is 1e-4).  At B >= 2048 the Riccati
+    kernel runs its DPP-pivot variant and at B <= 128 its two-wave variant, with the four-wave
+    line search at B <= 256, so these are those variants' checks at their own sizes."""
     from oracle import cpu
 
-    B = 4096
-    xcur, goals, XU = synthetic_batch(B, N, seed=45 + N)
+    xcur, goals, XU = synthetic_batch(B, N, seed=seed)
     h = lib.Handle(model, N=N, max_batch=B)
     out, st = h.solve(xcur, goals, XU)
     ref, qp, al, _ = cpu.solve(xcur, goals, XU, N, nthreads=min(16, os.cpu_count() or 1))
