@@ -26,6 +26,7 @@ def test_ranks_on_shards_equal_single_process(world, batch):
     assert res["ranges"][0][0] == 0 and res["ranges"][-1][1] == batch
 
 
+@pytest.mark.timeout(540)
 def test_config5_eight_shards_equal_single_handle_and_port():
     """SURVEY.md §8d config 5 (B = 32768, N = 32, seed 47) as 8 ranks x 4096 — bench.py's
     `--gpus 8` sharding — here all on the one GPU: the concatenated shards equal one B = 32768

@@ -6,7 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${TAG:-run}
-STEPS=${STEPS:-tests,bench,trace,pmc,c4,fused}
+STEPS=${STEPS:-tests,bench,multi,trace,pmc,c4,fused}
 mkdir -p $O
 cd $R
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
@@ -17,6 +17,11 @@ fi
 if has bench; then
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 2; }
   cat $O/bench.json
+fi
+if has multi; then
+  # bench.py --gpus 2 starting its own ranks, both on the one GPU (--share-devices rehearsal)
+  timeout -k 10 300 python bench.py --gpus 2 --share-devices --steps 20 > $O/bench_g2.json 2> $O/bench_g2.err || { tail -20 $O/bench_g2.err; exit 13; }
+  cat $O/bench_g2.json
 fi
 cd /tmp
 if has trace; then
