@@ -70,7 +70,7 @@ class i7m_config(C.Structure):
         ("box_max_iters", C.c_int32),
         ("box_tol", C.c_double),
         ("pipeline", C.c_int32),
-        ("pad", C.c_int32),
+        ("h2h_chunks", C.c_int32),
     ]
 
 
@@ -194,7 +194,7 @@ class Handle:
 
     def __init__(self, model, N=32, dt=0.01, dQ_cost=0.01, R_cost=1e-5, QN_cost=100.0, regularize=True, eps=1.0,
                  max_batch=1, device_id=0, mu=10.0, step_tol=1e-3, max_sqp_iters=2, qp_mode=QP_DIRECT,
-                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8, pipeline=PIPE_AUTO):
+                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8, pipeline=PIPE_AUTO, h2h_chunks=0):
         lib = load()
         cfg = i7m_config()
         _check(lib.i7m_config_default(C.byref(cfg)))
@@ -203,6 +203,7 @@ class Handle:
         cfg.max_sqp_iters, cfg.max_batch, cfg.device_id = int(max_sqp_iters), int(max_batch), int(device_id)
         cfg.qp_mode, cfg.box_mask, cfg.box_max_iters, cfg.box_tol = int(qp_mode), int(box_mask), int(box_max_iters), float(box_tol)
         cfg.pipeline = int(pipeline)
+        cfg.h2h_chunks = int(h2h_chunks)
         packed = np.ascontiguousarray(model.packed(), dtype=np.float64)
         assert packed.nbytes == C.sizeof(i7m_model), (packed.nbytes, C.sizeof(i7m_model))
         C.memmove(C.byref(cfg.model), packed.ctypes.data, packed.nbytes)

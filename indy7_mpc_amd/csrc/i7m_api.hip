@@ -119,6 +119,11 @@ struct i7m_handle {
   int pipeline = I7M_PIPE_AUTO;  // cfg.pipeline, or I7M_PIPE=split|fused
   int ric_w2 = -1;               // k_riccati_mfma_w2 (two waves per problem): 1 / 0, -1 = by batch size
   int ric_bc = -1;               // k_riccati_mfma broadcast variant (BC bits), -1 = by batch size
+  // host-to-host i7m_solve split into chunks on two streams, so the copies of one chunk overlap
+  // the solve of another (0 = one piece on h->stream; I7M_H2H_CHUNKS or cfg.h2h_chunks)
+  int h2h_chunks = 0;
+  hipStream_t cs[2] = {nullptr, nullptr};
+  hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -433,7 +438,7 @@ bool use_fused(const i7m_handle* h, int B) {
 
 
 int launch_fused(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu_in, double* xu_out,
-                 const double* xs, const double* goals, ProblemStats* st) {
+                 const double* xs, const double* goals, ProblemStats* st, long b0) {
   const int nw = waves_for(h, P.B);
   // I7M_PIPE_FUSED_ITER: one launch per SQP iteration, else one per solve
   const int launches = h->pipeline == I7M_PIPE_FUSED_ITER ? h->cfg.max_sqp_iters : 1;
@@ -442,7 +447,7 @@ int launch_fused(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams&
     const int rc = timed(h, s, I7M_K_SQP_FUSED, [&](hipEvent_t ea, hipEvent_t eb) {
       e = i7m_launch_sqp_fused(h->spec, nw, h->fext_frame == I7M_WRENCH_WORLD, launches > 1 ? i : -1, s, ea, eb, h->d_model,
                                &P, i == 0 ? xu_in : xu_out, xu_out, xs, goals, W.fext, W.lin, W.cost, W.qpd, W.kbuf,
-                               h->d_sol, h->d_active, st);
+                               h->d_sol + b0 * P.T, h->d_active + b0, st);
     });
     if (rc) return rc;
     if (e != hipSuccess) return fail(I7M_EHIP, std::string("k_sqp_fused launch: ") + hipGetErrorString(e));
@@ -453,25 +458,29 @@ int launch_fused(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams&
 // The SQP loop on device buffers: iteration 1 reads xu_in and its line search writes every
 // row of xu_out; later iterations update xu_out in place (xu_in == xu_out is allowed).  The
 // first linearisation also initialises the active flags and the stats (no memset launches).
-// (Splitting the batch into ranges on several streams, so that waves of different kernels share
-// a SIMD, was measured at 2-4 ranges and gave nothing: DESIGN.md §7.)
+// The B problems use the handle's per-problem work buffers from problem b0 on, and run on
+// stream s (h->stream unless the host-to-host path splits the batch into chunks).
+// (Splitting a device-resident batch into ranges on several streams, so that waves of different
+// kernels share a SIMD, was measured at 2-4 ranges and gave nothing: DESIGN.md §7.)
 int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const double* d_xs, const double* d_goals,
-            int goal_stride, ProblemStats* d_st) {
-  const Bufs W = bufs_at(h, 0);
+            int goal_stride, ProblemStats* d_st, long b0 = 0, hipStream_t s = nullptr) {
+  const Bufs W = bufs_at(h, b0);
   const SolveParams P = params_of(h, B, goal_stride);
-  hipStream_t s = h->stream;
-  if (use_fused(h, B)) return launch_fused(h, s, W, P, d_xu_in, d_xu, d_xs, d_goals, d_st);
+  if (!s) s = h->stream;
+  int* act = h->d_active + b0;
+  double* qbuf = h->d_sol + b0 * P.T;
+  if (use_fused(h, B)) return launch_fused(h, s, W, P, d_xu_in, d_xu, d_xs, d_goals, d_st, b0);
   for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
     const double* xin = it == 0 ? d_xu_in : d_xu;
     int rc;
     if (it == 0)
-      rc = launch_linearize(h, s, W, P, xin, d_goals, nullptr, h->d_active, d_st);
+      rc = launch_linearize(h, s, W, P, xin, d_goals, nullptr, act, d_st);
     else
-      rc = launch_linearize(h, s, W, P, xin, d_goals, h->d_active);
+      rc = launch_linearize(h, s, W, P, xin, d_goals, act);
     if (rc) return rc;
     const double* qsol = nullptr;
-    if ((rc = solve_qp(h, s, W, P, xin, d_xs, h->d_active, h->d_sol, &qsol))) return rc;
-    if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, h->d_active, d_st, nullptr, it, 0,
+    if ((rc = solve_qp(h, s, W, P, xin, d_xs, act, qbuf, &qsol))) return rc;
+    if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, act, d_st, nullptr, it, 0,
                                 h->ablate != 6)))
       return rc;
   }
@@ -526,12 +535,55 @@ int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, c
   return I7M_OK;
 }
 
-int copy_in(i7m_handle* h, double* dst, const double* src, size_t n) {
-  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+// chunks of a host-to-host solve of B problems: the handle's setting, else automatic
+// (H2H_AUTO_CHUNKS from H2H_AUTO_MIN_B problems on; DESIGN.md §5 has the A/B)
+constexpr int H2H_AUTO_CHUNKS = 1;
+constexpr int H2H_AUTO_MIN_B = 1024;
+int h2h_chunks_for(const i7m_handle* h, int B) {
+  if (h->h2h_chunks > 0) return h->h2h_chunks;
+  return B >= H2H_AUTO_MIN_B ? H2H_AUTO_CHUNKS : 1;
+}
+
+int copy_in(i7m_handle* h, double* dst, const double* src, size_t n, hipStream_t s = nullptr) {
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, s ? s : h->stream));
   return I7M_OK;
 }
-int copy_out(i7m_handle* h, double* dst, const double* src, size_t n) {
-  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+int copy_out(i7m_handle* h, double* dst, const double* src, size_t n, hipStream_t s = nullptr) {
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, s ? s : h->stream));
+  return I7M_OK;
+}
+
+// Host-to-host solve in `nch` contiguous chunks of the batch, alternating over two streams: each
+// chunk is H2D of its rows -> its SQP -> D2H of its rows and stats, so chunk i's solve runs while
+// chunk i+1 is copied in and chunk i-1 copied out (PCIe is full duplex), instead of copy-in,
+// solve, copy-out back to back.  Ordered after earlier work on h->stream; synchronous.
+int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals, int goal_stride,
+                      double* xu_out, i7m_problem_stats* stats, int nch) {
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  int rc;
+  HIPCHK(hipEventRecord(h->ev_order, h->stream));
+  for (int c = 0; c < 2; ++c) HIPCHK(hipStreamWaitEvent(h->cs[c], h->ev_order, 0));
+  for (int i = 0; i < nch; ++i) {
+    const long lo = (long)B * i / nch, hi = (long)B * (i + 1) / nch;
+    const int n = (int)(hi - lo);
+    if (n == 0) continue;
+    hipStream_t s = h->cs[i & 1];
+    double* dxu = h->d_xu + lo * T;
+    double* dxs = h->d_xs + lo * 12;
+    double* dg = h->d_goal + lo * N * goal_stride;
+    if ((rc = copy_in(h, dxu, xu_in + lo * T, n * T, s))) return rc;
+    if ((rc = copy_in(h, dxs, xcur + lo * 12, (size_t)n * 12, s))) return rc;
+    if ((rc = copy_in(h, dg, goals + lo * N * goal_stride, n * N * goal_stride, s))) return rc;
+    if ((rc = run_sqp(h, n, dxu, dxu, dxs, dg, goal_stride, h->d_stats + lo, lo, s))) return rc;
+    if ((rc = copy_out(h, xu_out + lo * T, dxu, n * T, s))) return rc;
+    if (stats)
+      HIPCHK(hipMemcpyAsync(stats + lo, h->d_stats + lo, sizeof(ProblemStats) * (size_t)n, hipMemcpyDeviceToHost, s));
+  }
+  for (int c = 0; c < 2; ++c) {
+    HIPCHK(hipEventRecord(h->ev_done[c], h->cs[c]));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[c], 0));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
 }
 
@@ -641,6 +693,15 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     const int v = std::atoi(e) & 7;
     h->ric_bc = (v == 4 || v == 5) ? (v & 3) : v;  // instantiated: 0 1 2 3 6 7
   }
+  h->h2h_chunks = cfg->h2h_chunks;
+  if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
+  if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
+  if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_order, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_done[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_done[1], hipEventDisableTiming) != hipSuccess)
+    return bail(fail(I7M_EHIP, "chunk stream / event creation failed"));
   h->pipeline = cfg->pipeline;
   if (const char* e = std::getenv("I7M_PIPE"))
     h->pipeline = std::strcmp(e, "fused") == 0 ? I7M_PIPE_FUSED
@@ -697,6 +758,14 @@ void i7m_destroy(i7m_handle* h) {
   }
   for (auto e : h->pool) (void)hipEventDestroy(e);
   drop_graphs(h);
+  for (int c = 0; c < 2; ++c) {
+    if (h->cs[c]) {
+      (void)hipStreamSynchronize(h->cs[c]);
+      (void)hipStreamDestroy(h->cs[c]);
+    }
+    if (h->ev_done[c]) (void)hipEventDestroy(h->ev_done[c]);
+  }
+  if (h->ev_order) (void)hipEventDestroy(h->ev_order);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
@@ -761,6 +830,8 @@ int i7m_solve(i7m_handle* h, int32_t B, const double* xu_in, const double* xcur,
   if (!xu_in || !xcur || !goals || !xu_out) return fail(I7M_EINVAL, "null pointer");
   HIPCHK(hipSetDevice(h->dev));
   const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  const int nch = std::min(h2h_chunks_for(h, B), B);
+  if (nch > 1) return solve_h2h_chunked(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch);
   if ((rc = copy_in(h, h->d_xu, xu_in, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;

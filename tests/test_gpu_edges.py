@@ -295,3 +295,24 @@ def test_fused_device_solve_out_of_place(lib, model):
         np.testing.assert_array_equal(t_xu.cpu().numpy(), XU)
         st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=lib.STATS_DTYPE)
         np.testing.assert_array_equal(st["alphas"], st_ref["alphas"])
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 7])
+def test_chunked_host_to_host_solve_bit_identical(lib, model, chunks):
+    """i7m_solve split into chunks on two streams (h2h_chunks, copies overlapping solves) gives
+    the one-piece solve's XU and stats bit for bit, also for chunks that do not divide B."""
+    from oracle.osqp_ref import synthetic_batch
+
+    B, N = 300, 32
+    xcur, goals, XU = synthetic_batch(B, N, seed=71)
+    h1 = lib.Handle(model, N=N, max_batch=B, h2h_chunks=1)
+    hc = lib.Handle(model, N=N, max_batch=B, h2h_chunks=chunks)
+    o1, s1 = h1.solve(xcur, goals, XU)
+    oc, sc = hc.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(oc, o1)
+    assert np.array_equal(sc, s1)
+    # a smaller batch than the handle's, and B < chunks
+    o1, s1 = h1.solve(xcur[:5], goals[:5], XU[:5])
+    oc, sc = hc.solve(xcur[:5], goals[:5], XU[:5])
+    np.testing.assert_array_equal(oc, o1)
+    assert np.array_equal(sc, s1)

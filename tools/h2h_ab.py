@@ -1,0 +1,54 @@
+"""A/B of the host-to-host solve (i7m_solve: numpy in, numpy out) split into chunks on two
+streams (i7m_config.h2h_chunks) at config 3 (B = 4096, N = 32): median of 20 timed calls after 3
+warm-up calls per chunk count (BASELINE.md §4's procedure), each output checked bit for bit
+against the one-piece solve.  Prints one JSON line per setting.
+
+    python tools/h2h_ab.py [--batch 4096] [--N 32] [--chunks 1,2,3,4,8] [--reps 20]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--chunks", default="1,2,3,4,8")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import numpy as np
+
+    from indy7_mpc_amd import _lib
+    from indy7_mpc_amd.model import default_model
+    from indy7_mpc_amd.synthetic import make_batch
+
+    model = default_model()
+    ref = None
+    for nch in [int(c) for c in a.chunks.split(",")]:
+        h = _lib.Handle(model, N=a.N, max_batch=a.batch, h2h_chunks=nch)
+        xcur, goals, XU = make_batch(h, model, a.batch, a.N, 45)
+        ts = []
+        for i in range(a.reps + 3):
+            t0 = time.perf_counter()
+            out, st = h.solve(xcur, goals, XU)
+            if i >= 3:
+                ts.append(time.perf_counter() - t0)
+        if ref is None:
+            ref = (out, st)
+        same = bool(np.array_equal(out, ref[0]) and np.array_equal(st, ref[1]))
+        med = statistics.median(ts)
+        print(json.dumps({"h2h_chunks": nch, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
+                          "host_to_host_solves_per_s": a.batch / med, "min_ms": 1e3 * min(ts),
+                          "bit_identical_to_first": same}), flush=True)
+        h.close()
+
+
+if __name__ == "__main__":
+    main()
