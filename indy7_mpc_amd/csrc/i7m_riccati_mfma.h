@@ -47,10 +47,113 @@ enum : int {
   MO_ONE = 369,
   MO_GJ = 370,   // 6 x 40  per-pivot Gauss-Jordan exchange slots (diagnostic variant)
   MO_DUMMY = MO_GJ,  // 64: lane l's sink for the stores it has nothing to write (branch-free)
-  MO_TOTAL = 610,
-  MO_QX = 610,   // 256  two-wave body: Qxx~ of wave 1 in the accumulator layout (64 i + lane)
-  MO_TOTAL_W2 = 866,
+  // 4x4-block products (S44): V~'s v-v block, W = V_vv Bu, W0's v rows (all 6 x 6 / 6 x 13 row-major)
+  MO_VV = 610,
+  MO_WV = 646,
+  MO_W0V = 682,
+  MO_TOTAL = 760,
+  MO_QX = 760,   // 256  two-wave body: Qxx~ of wave 1 in the accumulator layout (64 i + lane)
+  MO_TOTAL_W2 = 1016,
 };
+
+// I7M_RIC_44 (default 1): the stage's small products — H = Bu V_vv Bu + R and G~ = Bu W0_v + N~
+// — on v_mfma_f64_4x4x4_4b blocks instead of padded 16x16x4 MFMAs.  On gfx950
+// fp64 MFMA and fp64 VALU share one rate, and the 4x4x4_4b form retires FMAs at the 16x16x4 rate
+// (tools/probes/fp64_pipes.hip), so an MFMA costs its padded size: H's two 16x16x4 steps (128
+// cycles) did 216 useful FMAs of 2048, W1 = V B~ and G~ 23 % each.  As blocks: W (2 instructions),
+// H (2), G~ (4) = 128 cycles for what took 384.  Different summation grouping than the 16x16
+// form, so the two builds differ by rounding (both within the parity tolerances); every variant
+// (one wave, two waves, k_sqp_fused) uses the same one, so they stay bit-identical to each other.
+#ifndef I7M_RIC_44
+#define I7M_RIC_44 1
+#endif
+
+// v_mfma_f64_4x4x4_4b: four independent 4 x 4 x 4 blocks.  Lane layouts (gfx950, probed by
+// tools/probes/mfma_f64_4x4_layout.hip): A lane 16k + 4s + i = A_s[i][k], B lane 16k + 4s + j =
+// B_s[k][j], D lane 16i + 4s + j = D_s[i][j] — the 16x16x4 operand layouts with the 4 x 4
+// diagonal blocks of the product as results.  Block s of a 2 x 2 block product takes (row block,
+// column block) = (s & 1, (s ^ (s >> 1)) & 1): 0 (0,0), 1 (1,1), 2 (0,1), 3 (1,0).
+__device__ __forceinline__ double mfma44(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int blk_r(int s) { return s & 1; }
+__device__ __forceinline__ int blk_c(int s) { return (s ^ (s >> 1)) & 1; }
+
+// Per-lane LDS offsets of the 4x4-block products (fixed for the kernel).  Invalid (padding)
+// entries read MO_ZERO; results with nothing to store go to the lane's sink slot.
+struct Ric44Maps {
+  int wA[2], wB[2], wD;        // W = V_vv Bu          (k-steps 0, 1)
+  int hA[2], hB[2], hD, hR;    // H = Bu' W + R        (hR: Rm on the diagonal, else 0)
+  int gA[2][2], gB[2], gD[2], gN[2];  // G~ = Bu W0_v + N~, row block rb = 0, 1 (gN: r in column 12)
+  int oGB[2];                  // G~ in the 16x16x4 B layout (k-step s: G~[4s + lq][lr]) for V~'s update
+  int vvS[2], w0S[2];          // stores of V~'s v-v block (V[1], V[2]) and W0's v rows (W0[1], W0[2])
+};
+__device__ __forceinline__ Ric44Maps ric44_maps(const int l) {
+  Ric44Maps M;
+  const int hi = l >> 4, s = (l >> 2) & 3, lo = l & 3, lq = l >> 4, lr = l & 15;
+  const int rA = 4 * blk_r(s) + lo, cB = 4 * blk_c(s) + lo;   // A row / B column of this lane
+  const int rD = 4 * blk_r(s) + hi, cD = 4 * blk_c(s) + lo;   // D element of this lane
+  const int sink = MO_DUMMY + l;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int k = 4 * ks + hi;  // this lane's k in the A and B layouts
+    M.wA[ks] = (rA < 6 && k < 6) ? MO_VV + 6 * rA + k : MO_ZERO;
+    M.wB[ks] = (k < 6 && cB < 6) ? MO_BU + 6 * k + cB : MO_ZERO;
+    M.hA[ks] = (rA < 6 && k < 6) ? MO_BU + 6 * k + rA : MO_ZERO;  // Bu' [rA][k]
+    M.hB[ks] = (k < 6 && cB < 6) ? MO_WV + 6 * k + cB : MO_ZERO;
+    M.gB[ks] = (k < 6 && 4 * s + lo < 13) ? MO_W0V + 13 * k + 4 * s + lo : MO_ZERO;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int r = 4 * rb + lo;  // Bu' [r][k] = Bu[k][r]
+      M.gA[rb][ks] = (r < 6 && k < 6) ? MO_BU + 6 * k + r : MO_ZERO;
+    }
+    M.oGB[ks] = (4 * ks + lq < 6 && lr < 13) ? MO_G + 13 * (4 * ks + lq) + lr : MO_ZERO;
+  }
+  M.wD = (rD < 6 && cD < 6) ? MO_WV + 6 * rD + cD : sink;
+  M.hD = (rD < 6 && cD < 6) ? MO_H + 6 * rD + cD : sink;
+  M.hR = (rD == cD && rD < 6) ? MO_RM : MO_ZERO;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = 4 * rb + hi, c = 4 * s + lo;
+    M.gD[rb] = (r < 6 && c < 13) ? MO_G + 13 * r + c : sink;
+    M.gN[rb] = (r < 6 && c == 12) ? MO_LU + r : MO_ZERO;
+  }
+  // V~ (accumulator layout: register i holds row lq + 4i of column lr): rows 6..11 are register 1
+  // (lq = 2, 3) and register 2 (all lq); V_vv takes columns 6..11, W0_v columns 0..12.
+  // V_vv is stored TRANSPOSED: the 16x16 products take V~'s accumulator registers as their A
+  // operand, i.e. they use V~' (W0 = V~' A~, the old W1 = V~' B~).  V~ = Qxx + K~'G~ is symmetric
+  // only to the accuracy of K~ = -H^-1 G~, and H can be very ill-conditioned (R = 1e-5 w against
+  // Bu' V Bu), so H = Bu' (V~')_vv Bu keeps the recursion on the one matrix V~' throughout — with
+  // V~_vv instead, 1e-8 relative errors at N = 32 and 1e-4 at N = 64 (measured).
+  M.vvS[0] = (lq >= 2 && lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq - 2) : sink;
+  M.vvS[1] = (lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq + 2) : sink;
+  M.w0S[0] = (lq >= 2 && lr < 13) ? MO_W0V + 13 * (lq - 2) + lr : sink;
+  M.w0S[1] = (lr < 13) ? MO_W0V + 13 * (lq + 2) + lr : sink;
+  return M;
+}
+// W = V_vv Bu, then H = Bu' W + R into MO_H (needs V_vv, Bu, Rm in LDS; one wave)
+__device__ __forceinline__ void ric44_h(const Ric44Maps& M, double* __restrict__ sh) {
+  double w = 0.0;
+  w = mfma44(sh[M.wA[0]], sh[M.wB[0]], w);
+  w = mfma44(sh[M.wA[1]], sh[M.wB[1]], w);
+  sh[M.wD] = w;
+  wave_sync();
+  double h = sh[M.hR];
+  h = mfma44(sh[M.hA[0]], sh[M.hB[0]], h);
+  h = mfma44(sh[M.hA[1]], sh[M.hB[1]], h);
+  sh[M.hD] = h;
+}
+// G~ = Bu' W0_v + N~ into MO_G (needs W0_v, Bu, r in LDS; one wave)
+__device__ __forceinline__ void ric44_g(const Ric44Maps& M, double* __restrict__ sh) {
+  const double b0 = sh[M.gB[0]], b1 = sh[M.gB[1]];
+  double g0 = sh[M.gN[0]], g1 = sh[M.gN[1]];
+  g0 = mfma44(sh[M.gA[0][0]], b0, g0);
+  g1 = mfma44(sh[M.gA[1][0]], b0, g1);
+  g0 = mfma44(sh[M.gA[0][1]], b1, g0);
+  g1 = mfma44(sh[M.gA[1][1]], b1, g1);
+  sh[M.gD[0]] = g0;
+  sh[M.gD[1]] = g1;
+}
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -369,6 +472,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     oK[s] = (u < 6 && lr < 13) ? MO_KT + 13 * u + lr : MO_ZERO;
   }
 
+  // the small products on 4x4x4 blocks (I7M_RIC_44): plain QP only (the box body keeps the
+  // 16x16 forms; the diagnostic LDS-exchange elimination too)
+  constexpr bool S44 = I7M_RIC_44 && !BOX && !(ABL & 4);
+  const Ric44Maps M44 = ric44_maps(l);
   constexpr int SE = BOX ? 176 : 140;  // stash length
   // Branch-free lane-conditional stores (lanes with nothing to store write a per-lane sink slot,
   // DESIGN.md §7) in the plain QP only: in the box body (k_ipm_fused) the sink addresses and
@@ -433,6 +540,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         sh[MO_AQ + l] = p0;
         sh[MO_AQ + l + 64] = p1;
         sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
+        if constexpr (S44) {
+          sh[M44.vvS[0]] = V[1];
+          sh[M44.vvS[1]] = V[2];
+        }
       }
       lds_sync();
       if (w == 0 && k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
@@ -443,13 +554,19 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       bB[1] = sh[offB[1]];
       d4 W0, Z00, Z10;
       if (w == 0) {
-        d4 Ni;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Ni[i] = sh[oN[i]];
 #pragma unroll
         for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
 #pragma unroll
         for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
+        if constexpr (S44) {
+          sh[M44.w0S[0]] = W0[1];
+          sh[M44.w0S[1]] = W0[2];
+          wave_sync();
+          ric44_g(M44, sh);
+        } else {
+        d4 Ni;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ni[i] = sh[oN[i]];
         Z10 = mfma(bB[0], W0[1], Ni);
         Z10 = mfma(bB[1], W0[2], Z10);
 #pragma unroll
@@ -457,6 +574,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
           const int r = lq + 4 * i;
           sh[(r < 6 && lr < 13) ? MO_G + 13 * r + lr : MO_DUMMY + l] = Z10[i];
         }
+        }
+      } else if (S44) {
+        ric44_h(M44, sh);
       } else {
         d4 Ri;
 #pragma unroll
@@ -514,8 +634,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       if (w == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) Z00[i] = sh[MO_QX + 64 * i + l];
-      } else {
-        // G~ as wave 0's accumulators held it (rows >= 6 and columns >= 13 are exact zeros there)
+      }
+      if (w != 0 || S44) {
+        // G~ as wave 0's accumulators held it (rows >= 6 and columns >= 13 are exact zeros there);
+        // S44: both waves (G~ came from 4x4 blocks, not from a 16x16 accumulator)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r = lq + 4 * i;
@@ -539,20 +661,28 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     sh[MO_AQ + l + 64] = p1;
     if (BF) sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
     else if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
+    if constexpr (S44) {  // V~'s v-v block for H = Bu' V_vv Bu (4x4 blocks)
+      sh[M44.vvS[0]] = V[1];
+      sh[M44.vvS[1]] = V[2];
+    }
     wave_sync();
     if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
     double bA[4], bB[2];
 #pragma unroll
     for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
-    bB[0] = sh[offB[0]];
-    bB[1] = sh[offB[1]];
     d4 Qi, Ri, Ni;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i)
       // (x + 0.0 is not folded for doubles: the box shifts are added only in BOX builds)
       Qi[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
-      Ri[i] = BOX ? sh[oR[i]] + sh[oR2[i]] : sh[oR[i]];
-      Ni[i] = BOX ? sh[oN[i]] + sh[oN2[i]] : sh[oN[i]];
+    if constexpr (!S44) {
+      bB[0] = sh[offB[0]];
+      bB[1] = sh[offB[1]];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Ri[i] = BOX ? sh[oR[i]] + sh[oR2[i]] : sh[oR[i]];
+        Ni[i] = BOX ? sh[oN[i]] + sh[oN2[i]] : sh[oN[i]];
+      }
     }
     // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
     // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
@@ -564,6 +694,18 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
     if (ABL & 512) tb = tstamp(W0[0] + W0[1] + W0[2] + W0[3]);
     d4 Z00 = Qi;
+    d4 Z10, Z11;
+    if constexpr (S44) {
+      // W0's v rows for G~; then H = Bu' V_vv Bu + R (under the Qxx chain), G~ = Bu' W0_v + N~,
+      // both stored into MO_H / MO_G for the elimination
+      sh[M44.w0S[0]] = W0[1];
+      sh[M44.w0S[1]] = W0[2];
+      ric44_h(M44, sh);
+      if (lq == 0) Z00[3] += W0[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+      ric44_g(M44, sh);
+    } else {
     if (lq == 0) Z00[3] += W0[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
@@ -571,12 +713,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     d4 W1 = {0.0, 0.0, 0.0, 0.0};
     W1 = mfma(V[1], bB[0], W1);
     W1 = mfma(V[2], bB[1], W1);
-    d4 Z11 = mfma(bB[0], W1[1], Ri);
+    Z11 = mfma(bB[0], W1[1], Ri);
     Z11 = mfma(bB[1], W1[2], Z11);
     if (ABL & 512) tm1 = tstamp(bA[0] + bA[1] + bA[2] + bA[3] + Qi[0] + Ri[0] + Ni[0]);
-    d4 Z10 = mfma(bB[0], W0[1], Ni);
+    Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
     if (ABL & 512) tm2 = tstamp(Z10[0] + Z10[1] + Z11[0] + Z11[1]);
+    }
     double* kk = KB + (long)((ABL & 8) ? 0 : k) * KBUF_STRIDE;
     if ((ABL & 4) && !BOX) {
       // (Diagnostic alternative, I7M_ABLATE=8: measured 5 us slower per launch at B = 1 and
@@ -635,6 +778,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       // columns: row 0 = H 0..5, G~ 0..9; row 1 = H 0..5 again, G~ 10..12 and (HINV) the
       // identity columns, which end as H^-1.  The two copies of H evolve identically.
       // (stores of lanes with nothing to store go to their own dummy slot: no exec-mask branches)
+      if constexpr (!S44) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r = lq + 4 * i;
@@ -646,7 +790,12 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
           if (lr < 13) sh[MO_G + 13 * r + lr] = Z10[i];
         }
       }
+      }
       wave_sync();
+      if constexpr (S44) {  // G~ in the 16x16x4 B layout for V~'s update below
+        Z10[0] = sh[M44.oGB[0]];
+        Z10[1] = sh[M44.oGB[1]];
+      }
       double E[6];
       // column of lane l: 0..5 H, 6..18 G~, 19..24 identity (HINV); -1 unused (rows 2, 3 and
       // row 1's tail compute a copy of H column 0 and store nothing)
