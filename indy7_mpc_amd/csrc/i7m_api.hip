@@ -122,6 +122,7 @@ struct i7m_handle {
   // host-to-host i7m_solve split into chunks on two streams, so the copies of one chunk overlap
   // the solve of another (0 = one piece on h->stream; I7M_H2H_CHUNKS or cfg.h2h_chunks)
   int h2h_chunks = 0;
+  int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   hipStream_t cs[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
   // timing
@@ -695,6 +696,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   }
   h->h2h_chunks = cfg->h2h_chunks;
   if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
+  if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||
@@ -819,6 +821,24 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
   HIPCHK(hipSetDevice(h->dev));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
+  if (h->dev_ranges > 1 && B >= h->dev_ranges) {
+    // A/B knob (I7M_DEV_RANGES): the batch as contiguous ranges on the two chunk streams, so one
+    // range's kernels can fill the SIMDs another range's kernel tail leaves idle
+    const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+    HIPCHK(hipEventRecord(h->ev_order, h->stream));
+    for (int c = 0; c < 2; ++c) HIPCHK(hipStreamWaitEvent(h->cs[c], h->ev_order, 0));
+    for (int i = 0; i < h->dev_ranges; ++i) {
+      const long lo = (long)B * i / h->dev_ranges, hi = (long)B * (i + 1) / h->dev_ranges;
+      if ((rc = run_sqp(h, (int)(hi - lo), d_xu_in + lo * T, d_xu_out + lo * T, d_xcur + lo * 12,
+                        d_goals + lo * N * goal_stride, goal_stride, st + lo, lo, h->cs[i & 1])))
+        return rc;
+    }
+    for (int c = 0; c < 2; ++c) {
+      HIPCHK(hipEventRecord(h->ev_done[c], h->cs[c]));
+      HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[c], 0));
+    }
+    return I7M_OK;
+  }
   return run_sqp_graphed(h, B, d_xu_in, d_xu_out, d_xcur, d_goals, goal_stride, st);
 }
 

@@ -147,8 +147,8 @@ __device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveP
   return S;
 }
 
-// Predictor: dx_aff = y - x; affine step lengths and mu_aff; sigma*mu (-> S.smu); the
-// corrector's h.
+// Predictor: dx_aff = y - x; affine step lengths and mu_aff (one pass); sigma*mu (-> S.smu);
+// the corrector's h (a second pass).
 // Element passes run in chunks of IPM_U elements per lane: the chunk's operands are all loaded
 // (clamped addresses, no branches) before any is used, so one wave has IPM_U x (2..5) loads in
 // flight instead of waiting out the memory latency element by element.  The per-lane order of
@@ -167,7 +167,12 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
   const int l = threadIdx.x;
   const int T = P.T;
   const long o = (long)b * T;
-  double ap = 1.0, ad = 1.0;
+  // pass 1: dx_aff = y - x, the affine step lengths, and mu_aff from four sums of the same pass —
+  // the complementarity after the affine step is bilinear in (ap, ad):
+  //   (s_l + ap d)(z_l + ad dz_l) + (s_u - ap d)(z_u + ad dz_u)
+  //     = [s_l z_l + s_u z_u] + ad [s_l dz_l + s_u dz_u] + ap [d z_l - d z_u] + ap ad [d dz_l - d dz_u]
+  // (oracle/box_ipm.py forms it the same way; one pass over x, z_l, z_u instead of two)
+  double ap = 1.0, ad = 1.0, s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
   for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
     double yv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U];
 #pragma unroll
@@ -190,37 +195,23 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
           const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
           ap = ratio_min(ratio_min(ap, sl, d), su, -d);
           ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
+          s00 += sl * a + su * c;
+          s01 += sl * dzl + su * dzu;
+          s10 += d * a - d * c;
+          s11 += d * dzl - d * dzu;
         }
       }
     }
   }
   wave_min2(ap, ad);
-  double acc = 0.0;
-  for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
-    double dv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U];
-#pragma unroll
-    for (int u = 0; u < IPM_U; ++u) {
-      const int e = min(e0 + 64 * u, T - 1);
-      dv[u] = dxa[o + e];
-      xv[u] = x[o + e];
-      av[u] = zl[o + e];
-      cv[u] = zu[o + e];
-    }
-#pragma unroll
-    for (int u = 0; u < IPM_U; ++u) {
-      const int e = e0 + 64 * u;
-      double lo, hi;
-      if (e < T && box_of(Bt, e, lo, hi)) {
-        const double d = dv[u], xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
-        const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
-        acc += (sl + ap * d) * (a + ad * dzl) + (su - ap * d) * (c + ad * dzu);
-      }
-    }
-  }
-  acc = wave_sum(acc);
-  const double mua = acc / (2.0 * S.nb);
+  s00 = wave_sum(s00);
+  s01 = wave_sum(s01);
+  s10 = wave_sum(s10);
+  s11 = wave_sum(s11);
+  const double mua = ((s00 + ad * s01) + ap * (s10 + ad * s11)) / (2.0 * S.nb);
   const double r = mua / S.mu;
   const double smu = r * r * r * S.mu;
+  // pass 2: the corrector's linear-term shift h
   for (int e0 = l; e0 < T; e0 += 64 * IPM_U) {
     double dv[IPM_U], xv[IPM_U], av[IPM_U], cv[IPM_U], hold[IPM_U];
 #pragma unroll
@@ -467,7 +458,9 @@ k_ipm_fused(IpmFusedArgs args) {
     const SolveParams P = A->P;
     __syncthreads();
     if (!DELTA) {
-      riccati_mfma_body<0, true, false, 2>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l);
+      // the corrector (half 1) stores only K~'s feedforward column: its gain is the predictor's
+      riccati_mfma_body<0, true, false, 2>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
+                                           nullptr, half == 1);
     } else if (half == 0) {
       riccati_mfma_body<0, true, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
                                        A->hinv);

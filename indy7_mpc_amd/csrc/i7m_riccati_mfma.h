@@ -402,7 +402,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
                                                   double* __restrict__ kbuf, double* __restrict__ sol,
                                                   const double* __restrict__ bsig, const double* __restrict__ bh,
                                                   double* __restrict__ sh, const int l,
-                                                  double* __restrict__ hinv = nullptr) {
+                                                  double* __restrict__ hinv = nullptr, const bool kff_only = false) {
   static_assert(!W2 || (!BOX && !HINV && ABL == 0), "two-wave body: plain QP only");
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
@@ -853,9 +853,17 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
           o[7] = (double)(tm4 - tm3);  // V~ update
         }
       }
+      if (BOX && kff_only) {
+        // a corrector step of the interior point: same Hessian as the predictor's, so its gain K is
+        // bit for bit the one the predictor stored (each K~ column is eliminated on its own with
+        // H's pivots, and the hom row / column of V~ never enters the first twelve columns); only
+        // the feedforward column changes, and c_v does not
+        if (l < 6) kk[13 * l + 12] = sh[MO_KT + 13 * l + 12];
+      } else {
       kk[l] = sh[MO_KT + l];
       if (BF) kk[64 + l20] = sh[ko20];  // lanes >= 20 repeat the stores of lanes l % 20 (same values)
       else if (l < 20) kk[64 + l] = (l < 14) ? sh[MO_KT + 64 + l] : sh[MO_CV + (l - 14)];
+      }
     }
   }
 

@@ -117,7 +117,13 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
         dzua = np.where(bm, -zu + zu * dxa / su, 0.0)
         ap = min(_ratio(sl, dxa, bm), _ratio(su, -dxa, bm))
         ad = min(_ratio(zl, dzla, bm), _ratio(zu, dzua, bm))
-        mua = float(((sl + ap * dxa)[bm] @ (zl + ad * dzla)[bm] + (su - ap * dxa)[bm] @ (zu + ad * dzua)[bm]) / (2 * nb))
+        # the complementarity after the affine step is bilinear in (ap, ad): four sums
+        # (i7m_box.h ipm_pred_body forms it the same way, in the pass that finds ap, ad)
+        s00 = float(np.sum((sl * zl + su * zu)[bm]))
+        s01 = float(np.sum((sl * dzla + su * dzua)[bm]))
+        s10 = float(np.sum((dxa * zl - dxa * zu)[bm]))
+        s11 = float(np.sum((dxa * dzla - dxa * dzua)[bm]))
+        mua = ((s00 + ad * s01) + ap * (s10 + ad * s11)) / (2 * nb)
         smu = (mua / mu) ** 3 * mu
         # corrector
         rl = np.where(bm, sl * zl + dxa * dzla - smu, 0.0)

@@ -1,6 +1,7 @@
-"""A/B of the config-4 interior-point paths on one GPU: k_ipm_fused<false> (default),
-k_ipm_fused<true> (I7M_IPM=delta: the corrector reuses the predictor's factorisation) and the
-split launches (I7M_IPM=split).  Same inputs; solves/s of each and the output difference vs split.  python tools/config4_ab.py [--steps 3] [--B 4096] [--N 64]"""
+"""Config 4 (B = 4096, N = 64, box rows) on one GPU: solves/s, IPM iterations and per-kernel
+times of the library in I7M_LIB (k_ipm_fused; the split-launch and factorisation-reuse forms
+measured in round 2 were removed in round 3).
+    python tools/config4_ab.py [--steps 3] [--B 4096] [--N 64]"""
 import argparse
 import json
 import os
@@ -18,10 +19,6 @@ def run(mode, B, N, steps):
     from indy7_mpc_amd.model import default_model
     from indy7_mpc_amd.synthetic import make_batch
 
-    if mode in ("split", "delta"):
-        os.environ["I7M_IPM"] = mode
-    else:
-        os.environ.pop("I7M_IPM", None)
     model = default_model()
     dev = torch.device("cuda", 0)
     h = _lib.Handle(model, N=N, max_batch=B, device_id=0, qp_mode=_lib.QP_BOX)
@@ -59,19 +56,13 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--N", type=int, default=64)
-    ap.add_argument("--modes", default="fused,delta,split")
+    ap.add_argument("--modes", default="fused")
     a = ap.parse_args()
     res, outs = {}, {}
     modes = a.modes.split(",")
     for mode in modes:
         outs[mode], res[mode] = run(mode, a.B, a.N, a.steps)
         res[mode].pop("ipm_iters_hist")
-    ref = outs.get("split")
-    for mode in ([m for m in ("fused", "delta") if m in modes] if ref is not None else []):
-        d = outs[mode] - ref
-        res[mode]["vs_split"] = {"bit_identical": bool(np.array_equal(outs[mode], ref)),
-                                 "max_abs_diff": float(np.abs(d).max()),
-                                 "max_rel_per_problem": float((np.linalg.norm(d, axis=1) / np.linalg.norm(ref, axis=1)).max())}
     print(json.dumps(res, indent=1), flush=True)
 
 
