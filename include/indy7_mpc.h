@@ -234,7 +234,7 @@ int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* en
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,
-       I7M_K_SQP_FUSED = 6, I7M_K_COUNT = 7 };
+       I7M_K_SQP_FUSED = 6, I7M_K_LINESEARCH_TAIL = 7 /* second launch of a split line search */, I7M_K_COUNT = 8 };
 int i7m_set_timing(i7m_handle* h, int enable);
 /* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
 int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);

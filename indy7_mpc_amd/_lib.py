@@ -26,9 +26,11 @@ MAX_SQP = 8
 MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
-I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_SQP_FUSED = range(7)
-I7M_K_COUNT = 7
-KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused", "k_sqp_fused")
+(I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_SQP_FUSED,
+ I7M_K_LINESEARCH_TAIL) = range(8)
+I7M_K_COUNT = 8
+KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused", "k_sqp_fused",
+                "k_linesearch_tail")
 
 
 class I7MError(RuntimeError):
@@ -249,10 +251,17 @@ class Handle:
             out.append(xc)
         return out
 
-    def solve(self, xcur, goals, xu):
+    def solve(self, xcur, goals, xu, out=None, stats=None):
+        """out / stats: optional preallocated (B, T) float64 / (B,) STATS_DTYPE arrays (e.g. views
+        of pinned host memory, which the chunked host-to-host path can copy asynchronously)."""
         xu, goals, B, stride, xc = self._batch(xu, goals, xcur)
-        out = np.empty_like(xu)
-        st = np.zeros(B, dtype=STATS_DTYPE)
+        if out is None:
+            out = np.empty_like(xu)
+        elif out.shape != xu.shape or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float64 array shaped like XU")
+        st = np.zeros(B, dtype=STATS_DTYPE) if stats is None else stats
+        if st.shape != (B,) or st.dtype != STATS_DTYPE:
+            raise ValueError("stats must be a (B,) STATS_DTYPE array")
         _check(self._lib.i7m_solve(self._h, B, _ptr(xu), _ptr(xc), _ptr(goals), stride, _ptr(out),
                                    st.ctypes.data_as(C.c_void_p)))
         return out, st

@@ -115,7 +115,12 @@ struct i7m_handle {
   unsigned long long graph_clock = 0;
   bool use_graph = false;  // I7M_GRAPH=1: capture the solve once per buffer set, replay it
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
-  int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1 or 4)
+  int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1, 2 or 4)
+  // I7M_LS_TAIL = r > 0: split line search — the first launch (one wave per problem) stops after r
+  // rounds, a second launch with two waves per problem finishes the unresolved problems
+  int ls_tail = 0;
+  double* d_lsbase = nullptr;  // (max_batch) base merits handed to the second launch
+  int* d_lspend = nullptr;     // (max_batch) pending flags
   int pipeline = I7M_PIPE_AUTO;  // cfg.pipeline, or I7M_PIPE=split|fused
   int ric_w2 = -1;               // k_riccati_mfma_w2 (two waves per problem): 1 / 0, -1 = by batch size
   int ric_bc = -1;               // k_riccati_mfma broadcast variant (BC bits), -1 = by batch size
@@ -345,10 +350,38 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
   const double* ln = base_from_lin ? W.lin : nullptr;
   const double* cs = base_from_lin ? W.cost : nullptr;
   const bool fw = W.fext && h->fext_frame == I7M_WRENCH_WORLD;
+  if (h->ls_tail > 0 && nw == 1 && mode == 0 && base_from_lin) {
+    // split search: r rounds of one wave per problem, then two waves per problem
+    // for the problems that have not accepted a candidate
+    const int R = P.N >= 64 ? 1 : 64 / P.N;
+    const int c_split = 1 + R * h->ls_tail;
+    const long b0 = W.lin - h->d_lin;  // this range's first problem (bufs_at offsets lin by b0 (N-1) stride)
+    const long pb = b0 / ((long)(P.N - 1) * LIN_STRIDE);
+    const LsSplit first{0, c_split, h->d_lsbase + pb, h->d_lspend + pb};
+    const LsSplit second{c_split, 1 + NALPHA, h->d_lsbase + pb, h->d_lspend + pb};
+    int rc = timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
+      auto go = [&](auto kern) {
+        hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(64), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
+                              active, st, alpha_out, iter, mode, W.lin, W.cost, first);
+      };
+      if (h->spec) fw ? go(k_linesearch<true, 0, 1, true>) : go(k_linesearch<true, 0, 1>);
+      else fw ? go(k_linesearch<false, 0, 1, true>) : go(k_linesearch<false, 0, 1>);
+    });
+    if (rc) return rc;
+    const size_t lds2 = ls_lds_bytes(P.T, 2);
+    return timed(h, s, I7M_K_LINESEARCH_TAIL, [&](hipEvent_t ea, hipEvent_t eb) {
+      auto go = [&](auto kern) {
+        hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(128), lds2, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
+                              active, st, alpha_out, iter, mode, W.lin, W.cost, second);
+      };
+      if (h->spec) fw ? go(k_linesearch<true, 0, 2, true>) : go(k_linesearch<true, 0, 2>);
+      else fw ? go(k_linesearch<false, 0, 2, true>) : go(k_linesearch<false, 0, 2>);
+    });
+  }
   return timed(h, s, I7M_K_LINESEARCH, [&](hipEvent_t ea, hipEvent_t eb) {
     auto go = [&](auto kern, int threads) {
       hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(threads), lds, s, ea, eb, 0, h->d_model, P, xu, xu_out, sol, goals, W.fext,
-                            active, st, alpha_out, iter, mode, ln, cs);
+                            active, st, alpha_out, iter, mode, ln, cs, LsSplit{});
     };
 #ifdef I7M_DIAG
     if (h->ablate == 4 && nw == 1) {
@@ -359,6 +392,9 @@ int launch_linesearch(i7m_handle* h, hipStream_t s, const Bufs& W, const SolvePa
     if (nw == 4) {
       if (h->spec) fw ? go(k_linesearch<true, 0, 4, true>, 256) : go(k_linesearch<true, 0, 4>, 256);
       else fw ? go(k_linesearch<false, 0, 4, true>, 256) : go(k_linesearch<false, 0, 4>, 256);
+    } else if (nw == 2) {  // A/B only (I7M_LS_WAVES=2)
+      if (h->spec) fw ? go(k_linesearch<true, 0, 2, true>, 128) : go(k_linesearch<true, 0, 2>, 128);
+      else fw ? go(k_linesearch<false, 0, 2, true>, 128) : go(k_linesearch<false, 0, 2>, 128);
     } else {
       if (h->spec) fw ? go(k_linesearch<true, 0, 1, true>, 64) : go(k_linesearch<true, 0, 1>, 64);
       else fw ? go(k_linesearch<false, 0, 1, true>, 64) : go(k_linesearch<false, 0, 1>, 64);
@@ -687,7 +723,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
 #endif
   if (const char* e = std::getenv("I7M_IPM"))
     h->ipm_mode = std::strcmp(e, "split") == 0 ? 2 : (std::strcmp(e, "delta") == 0 ? 0 : 1);
-  if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : 1;
+  if (const char* e = std::getenv("I7M_LS_TAIL")) h->ls_tail = std::min(std::max(std::atoi(e), 0), 3);
+  if (const char* e = std::getenv("I7M_LS_WAVES")) h->ls_waves = std::atoi(e) == 4 ? 4 : (std::atoi(e) == 2 ? 2 : 1);
   if (const char* e = std::getenv("I7M_GRAPH")) h->use_graph = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_RIC_W2")) h->ric_w2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_RIC_BC")) {
@@ -726,7 +763,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
             alloc((void**)&h->d_qpd, Bm * (N - 1) * QPD_STRIDE * 8) &&
             alloc((void**)&h->d_out, scratch * 8) &&
             alloc((void**)&h->d_active, Bm * sizeof(int)) && alloc((void**)&h->d_stats, Bm * sizeof(ProblemStats)) &&
-            alloc((void**)&h->d_fext, Bm * 6 * 8);
+            alloc((void**)&h->d_fext, Bm * 6 * 8) && alloc((void**)&h->d_lsbase, Bm * 8) &&
+            alloc((void**)&h->d_lspend, Bm * sizeof(int));
   if (ok && cfg->qp_mode == I7M_QP_BOX)
     ok = alloc((void**)&h->d_bx, Bm * T * 8) && alloc((void**)&h->d_bzl, Bm * T * 8) &&
          alloc((void**)&h->d_bzu, Bm * T * 8) && alloc((void**)&h->d_bsig, Bm * T * 8) &&
@@ -749,7 +787,7 @@ void i7m_destroy(i7m_handle* h) {
   (void)hipSetDevice(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
-                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_qpd,
+                  h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_qpd, h->d_lsbase, h->d_lspend,
                   h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact,
                   h->d_bhinv, h->d_bdh};
   for (void* p : bufs)

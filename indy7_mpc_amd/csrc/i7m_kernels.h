@@ -225,6 +225,18 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
   }
 }
 
+// Line search in two launches (I7M_LS_TAIL): the first launch evaluates the
+// candidates below c_end only; a problem none of them accepts stores its base merit, raises
+// pending[b] and leaves XU, the stats and the break flag to the second launch, which evaluates
+// the rest (c_begin on, base merit from `base`) with several waves per problem.  The candidates'
+// merits and the first-accept rule are those of the one-launch search, so alphas are identical.
+struct LsSplit {
+  int c_begin = 0;            // first candidate of this launch (0: the whole search, base first)
+  int c_end = 1 + NALPHA;     // candidates [.., c_end) in this launch
+  double* base = nullptr;     // (B) base merits handed from the first launch to the second
+  int* pending = nullptr;     // (B) 1: the second launch finishes this problem
+};
+
 // W waves per problem (small batches, where the GPU is otherwise idle): wave w evaluates the
 // candidate slots c0 + w R .. c0 + w R + R - 1 of each round, so W R candidates per round (all
 // eight alphas in one round at N = 32, W = 4).  Same first-accept rule, same merits.
@@ -240,7 +252,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
                                                 const double* __restrict__ fext, int* __restrict__ active,
                                                 ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
                                                 int iter, int mode, const double* __restrict__ lin,
-                                                const double* __restrict__ cost) {
+                                                const double* __restrict__ cost, const LsSplit sp = LsSplit{}) {
   const int N = P.N;
   const int R = (N >= 64) ? 1 : 64 / N;
   const int slot = l / N;
@@ -319,7 +331,12 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     lds_sync();
   };
   int cstart = 0;
-  if (lin && !zero_step) {
+  if (sp.c_begin > 0) {
+    // the second launch of a split search: base merit from the first
+    if (l == 0 && w == 0) merit[0] = sp.base[b];
+    lds_sync();
+    cstart = sp.c_begin;
+  } else if (lin && !zero_step) {
     // base merit (src/osqp_sqp.py:52-55) from the linearisation of this XU: |e| (cost[9]) and
     // a = ABA(q, v, u) (lin[108..113]) per knot; slot 0 of the candidate layout
     const double* LB = lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -352,7 +369,8 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   }
   double base = 0.0;
   int found = zero_step ? 1 : -1;
-  for (int c0 = cstart; c0 < 1 + NALPHA && found < 0; c0 += R * W) {
+  const int c_end = sp.c_end < 1 + NALPHA ? sp.c_end : 1 + NALPHA;
+  for (int c0 = cstart; c0 < c_end && found < 0; c0 += R * W) {
     if (I7M_PRIO & 2) set_prio((c0 - cstart) / (R * W));  // later rounds first: the longest searches
     const int cw = c0 + w * R;  // this wave's first candidate of the round
     const int cand = cw + slot;
@@ -394,10 +412,19 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     }
     reduce_store(o, cw, true);
     base = merit[0];
-    for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R * W && cc < 1 + NALPHA; ++cc) {
+    for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R * W && cc < c_end; ++cc) {
       if (merit[cc] <= base) { found = cc; break; }
     }
     lds_sync();
+  }
+  if (sp.pending) {
+    // first launch of a split search: hand an unresolved problem to the second launch
+    const int pend = (found < 0 && c_end < 1 + NALPHA) ? 1 : 0;
+    if (l == 0 && w == 0) {
+      sp.pending[b] = pend;
+      if (pend) sp.base[b] = merit[0];
+    }
+    if (pend) return;
   }
   if (W > 1 && w != 0) return;  // one wave applies the step
   const double alpha = (found > 0) ? alphas[found - 1] : 0.0;
@@ -448,15 +475,17 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(I7M
                                                    int* __restrict__ active,
                                                    ProblemStats* __restrict__ stats, double* __restrict__ alpha_out,
                                                    int iter, int mode, const double* __restrict__ lin = nullptr,
-                                                   const double* __restrict__ cost = nullptr) {
+                                                   const double* __restrict__ cost = nullptr, const LsSplit sp = LsSplit{}) {
   I7M_TL(3);
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
+  // the second launch of a split search runs only the problems the first one handed over
+  if (sp.c_begin > 0 && !sp.pending[b]) return;
   extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
   __shared__ double merit[9];
   linesearch_body<SPEC, ABL, W, FW>(Mg, P, b, W > 1 ? (int)(threadIdx.x >> 6) : 0, threadIdx.x & 63, ls_dyn, merit, xu,
-                                    xu_out, sol, goals, fext, active, stats, alpha_out, iter, mode, lin, cost);
+                                    xu_out, sol, goals, fext, active, stats, alpha_out, iter, mode, lin, cost, sp);
 }
 
 // Merit pieces of a given XU (hooks for SQP_OSQP.eepos_cost / integrator_err).

@@ -316,3 +316,29 @@ def test_chunked_host_to_host_solve_bit_identical(lib, model, chunks):
     oc, sc = hc.solve(xcur[:5], goals[:5], XU[:5])
     np.testing.assert_array_equal(oc, o1)
     assert np.array_equal(sc, s1)
+
+
+@pytest.mark.parametrize("tail", ["1", "2", "3"])
+def test_split_line_search_bit_identical(lib, model, monkeypatch, tail):
+    """I7M_LS_TAIL=r: the line search as two launches — r rounds of one wave per problem, then
+    two waves per problem for the problems that have not accepted a candidate (base merit handed
+    over) — gives the one-launch search's alphas, stats and XU bit for bit (B = 300 > 256, so the
+    one-wave kernel is the reference; both wrench frames)."""
+    B, N = 300, 32
+    xcur, goals, XU = synthetic_batch(B, N, seed=90 + int(tail))
+    fx = np.random.default_rng(3).normal(0.0, 20.0, (B, 6))
+    outs = {}
+    for t in ("0", tail):
+        monkeypatch.setenv("I7M_LS_TAIL", t)
+        h = lib.Handle(model, N=N, max_batch=B)
+        outs[t] = [h.solve(xcur, goals, XU)]
+        h.set_external_wrench(fx, frame="world")
+        outs[t].append(h.solve(xcur, goals, XU))
+        h.close()
+    for (o0, s0), (o1, s1) in zip(outs["0"], outs[tail]):
+        np.testing.assert_array_equal(o1, o0)
+        assert np.array_equal(s1, s0)
+    # the split really happened: some problem needed more than the first launch's candidates
+    st = outs["0"][0][1]
+    used = np.arange(st["alphas"].shape[1])[None, :] < st["n_alphas"][:, None]
+    assert (used & (st["alphas"] < 0.5 ** (2 * int(tail) - 1))).any()
