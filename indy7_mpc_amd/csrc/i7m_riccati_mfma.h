@@ -79,45 +79,64 @@ __device__ __forceinline__ double mfma44(double a, double b, double c) {
 __device__ __forceinline__ int blk_r(int s) { return s & 1; }
 __device__ __forceinline__ int blk_c(int s) { return (s ^ (s >> 1)) & 1; }
 
-// Per-lane LDS offsets of the 4x4-block products (fixed for the kernel).  Invalid (padding)
-// entries read MO_ZERO; results with nothing to store go to the lane's sink slot.
+// Per-lane LDS offsets of the 4x4-block products (fixed for the kernel), two 16-bit offsets per
+// 32-bit word (lo | hi << 16), laundered once per stage (ric44_launder) so that the unpacked
+// offsets are formed where used rather than hoisted out of the stage loop — unpacked, the maps
+// held ~36 VGPRs across the loop.  Invalid (padding) entries read MO_ZERO; results with nothing
+// to store go to the lane's sink slot.  BOX: the interior point's Sigma_u joins H's diagonal and
+// its h_u G~'s last column (second C-input words hR2 / gN2).
 struct Ric44Maps {
-  int wA[2], wB[2], wD;        // W = V_vv Bu          (k-steps 0, 1)
-  int hA[2], hB[2], hD, hR;    // H = Bu' W + R        (hR: Rm on the diagonal, else 0)
-  int gA[2][2], gB[2], gD[2], gN[2];  // G~ = Bu W0_v + N~, row block rb = 0, 1 (gN: r in column 12)
-  int oGB[2];                  // G~ in the 16x16x4 B layout (k-step s: G~[4s + lq][lr]) for V~'s update
-  int vvS[2], w0S[2];          // stores of V~'s v-v block (V[1], V[2]) and W0's v rows (W0[1], W0[2])
+  unsigned wAB[2];   // W = V_vv' Bu: A | B of k-step ks
+  unsigned hAB[2];   // H = Bu' W + R: A | B of k-step ks
+  unsigned hDR;      // H's store | its C input (Rm on the diagonal, else MO_ZERO)
+  unsigned wDhR2;    // W's store | BOX: Sigma_u on H's diagonal (else MO_ZERO)
+  unsigned gA[2];    // G~ = Bu' W0_v + N~: A of row block 0 | row block 1, k-step ks
+  unsigned gB;       // B of k-step 0 | 1
+  unsigned gD;       // stores of row block 0 | 1
+  unsigned gN;       // C inputs (r in column 12) of row block 0 | 1
+  unsigned gN2;      // BOX: h_u in column 12 of row block 0 | 1
+  unsigned oGB;      // G~ in the 16x16x4 B layout (k-step s: G~[4s + lq][lr]) for V~'s update: s = 0 | 1
+  unsigned vvS;      // stores of V~'s v-v block: register 1 | register 2
+  unsigned w0S;      // stores of W0's v rows: register 1 | register 2
 };
+__device__ __forceinline__ unsigned pk16(int lo, int hi) { return (unsigned)lo | ((unsigned)hi << 16); }
+__device__ __forceinline__ int lo16(unsigned v) { return (int)(v & 0xffffu); }
+__device__ __forceinline__ int hi16(unsigned v) { return (int)(v >> 16); }
+template <bool BOX>
 __device__ __forceinline__ Ric44Maps ric44_maps(const int l) {
   Ric44Maps M;
   const int hi = l >> 4, s = (l >> 2) & 3, lo = l & 3, lq = l >> 4, lr = l & 15;
   const int rA = 4 * blk_r(s) + lo, cB = 4 * blk_c(s) + lo;   // A row / B column of this lane
   const int rD = 4 * blk_r(s) + hi, cD = 4 * blk_c(s) + lo;   // D element of this lane
   const int sink = MO_DUMMY + l;
+  int gB[2], oGB[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int k = 4 * ks + hi;  // this lane's k in the A and B layouts
-    M.wA[ks] = (rA < 6 && k < 6) ? MO_VV + 6 * rA + k : MO_ZERO;
-    M.wB[ks] = (k < 6 && cB < 6) ? MO_BU + 6 * k + cB : MO_ZERO;
-    M.hA[ks] = (rA < 6 && k < 6) ? MO_BU + 6 * k + rA : MO_ZERO;  // Bu' [rA][k]
-    M.hB[ks] = (k < 6 && cB < 6) ? MO_WV + 6 * k + cB : MO_ZERO;
-    M.gB[ks] = (k < 6 && 4 * s + lo < 13) ? MO_W0V + 13 * k + 4 * s + lo : MO_ZERO;
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const int r = 4 * rb + lo;  // Bu' [r][k] = Bu[k][r]
-      M.gA[rb][ks] = (r < 6 && k < 6) ? MO_BU + 6 * k + r : MO_ZERO;
-    }
-    M.oGB[ks] = (4 * ks + lq < 6 && lr < 13) ? MO_G + 13 * (4 * ks + lq) + lr : MO_ZERO;
+    M.wAB[ks] = pk16((rA < 6 && k < 6) ? MO_VV + 6 * rA + k : MO_ZERO, (k < 6 && cB < 6) ? MO_BU + 6 * k + cB : MO_ZERO);
+    M.hAB[ks] = pk16((rA < 6 && k < 6) ? MO_BU + 6 * k + rA : MO_ZERO,   // Bu' [rA][k]
+                     (k < 6 && cB < 6) ? MO_WV + 6 * k + cB : MO_ZERO);
+    gB[ks] = (k < 6 && 4 * s + lo < 13) ? MO_W0V + 13 * k + 4 * s + lo : MO_ZERO;
+    // Bu' [r][k] = Bu[k][r], row blocks 0 | 1
+    M.gA[ks] = pk16((lo < 6 && k < 6) ? MO_BU + 6 * k + lo : MO_ZERO, (4 + lo < 6 && k < 6) ? MO_BU + 6 * k + 4 + lo : MO_ZERO);
+    oGB[ks] = (4 * ks + lq < 6 && lr < 13) ? MO_G + 13 * (4 * ks + lq) + lr : MO_ZERO;
   }
-  M.wD = (rD < 6 && cD < 6) ? MO_WV + 6 * rD + cD : sink;
-  M.hD = (rD < 6 && cD < 6) ? MO_H + 6 * rD + cD : sink;
-  M.hR = (rD == cD && rD < 6) ? MO_RM : MO_ZERO;
+  M.gB = pk16(gB[0], gB[1]);
+  M.oGB = pk16(oGB[0], oGB[1]);
+  const bool dg = rD == cD && rD < 6;
+  M.wDhR2 = pk16((rD < 6 && cD < 6) ? MO_WV + 6 * rD + cD : sink, (BOX && dg) ? MO_SIG + 12 + rD : MO_ZERO);
+  M.hDR = pk16((rD < 6 && cD < 6) ? MO_H + 6 * rD + cD : sink, dg ? MO_RM : MO_ZERO);
+  int gD[2], gN[2], gN2[2];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
     const int r = 4 * rb + hi, c = 4 * s + lo;
-    M.gD[rb] = (r < 6 && c < 13) ? MO_G + 13 * r + c : sink;
-    M.gN[rb] = (r < 6 && c == 12) ? MO_LU + r : MO_ZERO;
+    gD[rb] = (r < 6 && c < 13) ? MO_G + 13 * r + c : sink;
+    gN[rb] = (r < 6 && c == 12) ? MO_LU + r : MO_ZERO;
+    gN2[rb] = (BOX && r < 6 && c == 12) ? MO_HB + 12 + r : MO_ZERO;
   }
+  M.gD = pk16(gD[0], gD[1]);
+  M.gN = pk16(gN[0], gN[1]);
+  M.gN2 = pk16(gN2[0], gN2[1]);
   // V~ (accumulator layout: register i holds row lq + 4i of column lr): rows 6..11 are register 1
   // (lq = 2, 3) and register 2 (all lq); V_vv takes columns 6..11, W0_v columns 0..12.
   // V_vv is stored TRANSPOSED: the 16x16 products take V~'s accumulator registers as their A
@@ -125,34 +144,44 @@ __device__ __forceinline__ Ric44Maps ric44_maps(const int l) {
   // only to the accuracy of K~ = -H^-1 G~, and H can be very ill-conditioned (R = 1e-5 w against
   // Bu' V Bu), so H = Bu' (V~')_vv Bu keeps the recursion on the one matrix V~' throughout — with
   // V~_vv instead, 1e-8 relative errors at N = 32 and 1e-4 at N = 64 (measured).
-  M.vvS[0] = (lq >= 2 && lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq - 2) : sink;
-  M.vvS[1] = (lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq + 2) : sink;
-  M.w0S[0] = (lq >= 2 && lr < 13) ? MO_W0V + 13 * (lq - 2) + lr : sink;
-  M.w0S[1] = (lr < 13) ? MO_W0V + 13 * (lq + 2) + lr : sink;
+  M.vvS = pk16((lq >= 2 && lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq - 2) : sink,
+               (lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq + 2) : sink);
+  M.w0S = pk16((lq >= 2 && lr < 13) ? MO_W0V + 13 * (lq - 2) + lr : sink, (lr < 13) ? MO_W0V + 13 * (lq + 2) + lr : sink);
   return M;
 }
-// W = V_vv Bu, then H = Bu' W + R into MO_H (needs V_vv, Bu, Rm in LDS; one wave)
+__device__ __forceinline__ void ric44_launder(Ric44Maps& M) {
+  asm volatile("" : "+v"(M.wAB[0]), "+v"(M.wAB[1]), "+v"(M.hAB[0]), "+v"(M.hAB[1]), "+v"(M.hDR), "+v"(M.wDhR2),
+               "+v"(M.gA[0]), "+v"(M.gA[1]), "+v"(M.gB), "+v"(M.gD), "+v"(M.gN), "+v"(M.gN2), "+v"(M.oGB), "+v"(M.vvS),
+               "+v"(M.w0S));
+}
+// W = V_vv' Bu, then H = Bu' W + R (+ Sigma_u) into MO_H (needs V_vv', Bu, Rm in LDS; one wave)
+template <bool BOX>
 __device__ __forceinline__ void ric44_h(const Ric44Maps& M, double* __restrict__ sh) {
   double w = 0.0;
-  w = mfma44(sh[M.wA[0]], sh[M.wB[0]], w);
-  w = mfma44(sh[M.wA[1]], sh[M.wB[1]], w);
-  sh[M.wD] = w;
+  w = mfma44(sh[lo16(M.wAB[0])], sh[hi16(M.wAB[0])], w);
+  w = mfma44(sh[lo16(M.wAB[1])], sh[hi16(M.wAB[1])], w);
+  sh[lo16(M.wDhR2)] = w;
   wave_sync();
-  double h = sh[M.hR];
-  h = mfma44(sh[M.hA[0]], sh[M.hB[0]], h);
-  h = mfma44(sh[M.hA[1]], sh[M.hB[1]], h);
-  sh[M.hD] = h;
+  double h = BOX ? sh[hi16(M.hDR)] + sh[hi16(M.wDhR2)] : sh[hi16(M.hDR)];
+  h = mfma44(sh[lo16(M.hAB[0])], sh[hi16(M.hAB[0])], h);
+  h = mfma44(sh[lo16(M.hAB[1])], sh[hi16(M.hAB[1])], h);
+  sh[lo16(M.hDR)] = h;
 }
-// G~ = Bu' W0_v + N~ into MO_G (needs W0_v, Bu, r in LDS; one wave)
+// G~ = Bu' W0_v + N~ (+ h_u) into MO_G (needs W0_v, Bu, r in LDS; one wave)
+template <bool BOX>
 __device__ __forceinline__ void ric44_g(const Ric44Maps& M, double* __restrict__ sh) {
-  const double b0 = sh[M.gB[0]], b1 = sh[M.gB[1]];
-  double g0 = sh[M.gN[0]], g1 = sh[M.gN[1]];
-  g0 = mfma44(sh[M.gA[0][0]], b0, g0);
-  g1 = mfma44(sh[M.gA[1][0]], b0, g1);
-  g0 = mfma44(sh[M.gA[0][1]], b1, g0);
-  g1 = mfma44(sh[M.gA[1][1]], b1, g1);
-  sh[M.gD[0]] = g0;
-  sh[M.gD[1]] = g1;
+  const double b0 = sh[lo16(M.gB)], b1 = sh[hi16(M.gB)];
+  double g0 = sh[lo16(M.gN)], g1 = sh[hi16(M.gN)];
+  if (BOX) {
+    g0 += sh[lo16(M.gN2)];
+    g1 += sh[hi16(M.gN2)];
+  }
+  g0 = mfma44(sh[lo16(M.gA[0])], b0, g0);
+  g1 = mfma44(sh[hi16(M.gA[0])], b0, g1);
+  g0 = mfma44(sh[lo16(M.gA[1])], b1, g0);
+  g1 = mfma44(sh[hi16(M.gA[1])], b1, g1);
+  sh[lo16(M.gD)] = g0;
+  sh[hi16(M.gD)] = g1;
 }
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -472,10 +501,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     oK[s] = (u < 6 && lr < 13) ? MO_KT + 13 * u + lr : MO_ZERO;
   }
 
-  // the small products on 4x4x4 blocks (I7M_RIC_44): plain QP only (the box body keeps the
-  // 16x16 forms; the diagnostic LDS-exchange elimination too)
-  constexpr bool S44 = I7M_RIC_44 && !BOX && !(ABL & 4);
-  const Ric44Maps M44 = ric44_maps(l);
+  // the small products on 4x4x4 blocks (I7M_RIC_44), the box body too (its Sigma_u / h_u join
+  // the C inputs); not the diagnostic LDS-exchange elimination
+  constexpr bool S44 = I7M_RIC_44 && !(ABL & 4);
+  Ric44Maps M44 = ric44_maps<BOX>(l);
   constexpr int SE = BOX ? 176 : 140;  // stash length
   // Branch-free lane-conditional stores (lanes with nothing to store write a per-lane sink slot,
   // DESIGN.md §7) in the plain QP only: in the box body (k_ipm_fused) the sink addresses and
@@ -534,6 +563,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     return (long long)__builtin_amdgcn_s_memtime();
   };
   for (int k = N - 2; k >= 0; --k) {
+    if constexpr (S44) ric44_launder(M44);
     if constexpr (W2) {
       lds_sync();  // every wave is done with the previous stage's LDS
       if (w == 0) {
@@ -541,8 +571,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         sh[MO_AQ + l + 64] = p1;
         sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
         if constexpr (S44) {
-          sh[M44.vvS[0]] = V[1];
-          sh[M44.vvS[1]] = V[2];
+          sh[lo16(M44.vvS)] = V[1];
+          sh[hi16(M44.vvS)] = V[2];
         }
       }
       lds_sync();
@@ -559,10 +589,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
         for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
         if constexpr (S44) {
-          sh[M44.w0S[0]] = W0[1];
-          sh[M44.w0S[1]] = W0[2];
+          sh[lo16(M44.w0S)] = W0[1];
+          sh[hi16(M44.w0S)] = W0[2];
           wave_sync();
-          ric44_g(M44, sh);
+          ric44_g<BOX>(M44, sh);
         } else {
         d4 Ni;
 #pragma unroll
@@ -576,7 +606,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         }
         }
       } else if (S44) {
-        ric44_h(M44, sh);
+        ric44_h<BOX>(M44, sh);
       } else {
         d4 Ri;
 #pragma unroll
@@ -662,8 +692,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     if (BF) sh[l + 128 < SE ? MO_AQ + l + 128 : MO_DUMMY + l] = p2;
     else if (l + 128 < SE) sh[MO_AQ + l + 128] = p2;
     if constexpr (S44) {  // V~'s v-v block for H = Bu' V_vv Bu (4x4 blocks)
-      sh[M44.vvS[0]] = V[1];
-      sh[M44.vvS[1]] = V[2];
+      sh[lo16(M44.vvS)] = V[1];
+      sh[hi16(M44.vvS)] = V[2];
     }
     wave_sync();
     if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
@@ -698,13 +728,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     if constexpr (S44) {
       // W0's v rows for G~; then H = Bu' V_vv Bu + R (under the Qxx chain), G~ = Bu' W0_v + N~,
       // both stored into MO_H / MO_G for the elimination
-      sh[M44.w0S[0]] = W0[1];
-      sh[M44.w0S[1]] = W0[2];
-      ric44_h(M44, sh);
+      sh[lo16(M44.w0S)] = W0[1];
+      sh[hi16(M44.w0S)] = W0[2];
+      ric44_h<BOX>(M44, sh);
       if (lq == 0) Z00[3] += W0[3];
 #pragma unroll
       for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
-      ric44_g(M44, sh);
+      ric44_g<BOX>(M44, sh);
     } else {
     if (lq == 0) Z00[3] += W0[3];
 #pragma unroll
@@ -793,8 +823,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       wave_sync();
       if constexpr (S44) {  // G~ in the 16x16x4 B layout for V~'s update below
-        Z10[0] = sh[M44.oGB[0]];
-        Z10[1] = sh[M44.oGB[1]];
+        Z10[0] = sh[lo16(M44.oGB)];
+        Z10[1] = sh[hi16(M44.oGB)];
       }
       double E[6];
       // column of lane l: 0..5 H, 6..18 G~, 19..24 identity (HINV); -1 unused (rows 2, 3 and

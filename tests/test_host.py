@@ -116,3 +116,17 @@ def test_stats_recording_layout():
     assert s["linesearch_alphas"]["values"] == [0.125, 0.015625, 1.0]
     assert s["sqp_stepsizes"]["values"] == [27.1, 2.8, 1e-4]
     assert set(s) == {"qp_iters", "linesearch_alphas", "sqp_stepsizes"}
+
+
+def test_bench_refuses_more_ranks_than_devices():
+    """bench.py --gpus N without a launcher starts N ranks itself only when N devices are
+    visible (or --share-devices asks for a rehearsal); here there is no GPU, so it refuses with
+    exit status 2 before starting anything (no silently shared devices)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "--share-devices" in r.stderr
