@@ -123,8 +123,9 @@ typedef struct i7m_config {
   int32_t box_max_iters;/* interior-point iterations per QP, default 30 */
   double box_tol;       /* stop when mu < tol and the residuals shrank by tol, default 1e-8 */
   int32_t pipeline;     /* I7M_PIPE_* (appended), default I7M_PIPE_AUTO */
-  int32_t h2h_chunks;   /* i7m_solve (host buffers): split the batch into this many chunks on two
-                           streams so copies overlap solves; 0 = automatic (was `pad`: same layout) */
+  int32_t h2h_chunks;   /* i7m_solve (host buffers): split the batch into this many chunks, copies in,
+                           solves and copies out pipelined on three streams so copies overlap
+                           solves; 0 = automatic (was `pad`: same layout) */
 } i7m_config;
 
 /* Per-problem SQP statistics (keys of SQP_OSQP.stats, src/osqp_sqp.py:7-11). */

@@ -130,6 +130,10 @@ struct i7m_handle {
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   hipStream_t cs[2] = {nullptr, nullptr};
   hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
+  // pipelined host-to-host chunks (h2h_pipe, default; I7M_H2H_PIPE=0: the two alternating streams):
+  // per chunk, copy-in done on cs[0] -> solve on the handle's stream -> copy-out on cs[1]
+  int h2h_pipe = 1;
+  std::vector<hipEvent_t> ev_in, ev_cmp;
   // timing
   bool timing = false;
   std::vector<Timing> ev;
@@ -574,8 +578,8 @@ int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, c
 
 // chunks of a host-to-host solve of B problems: the handle's setting, else automatic
 // (H2H_AUTO_CHUNKS from H2H_AUTO_MIN_B problems on; DESIGN.md §5 has the A/B)
-constexpr int H2H_AUTO_CHUNKS = 1;
-constexpr int H2H_AUTO_MIN_B = 1024;
+constexpr int H2H_AUTO_CHUNKS = 2;
+constexpr int H2H_AUTO_MIN_B = 2048;
 int h2h_chunks_for(const i7m_handle* h, int B) {
   if (h->h2h_chunks > 0) return h->h2h_chunks;
   return B >= H2H_AUTO_MIN_B ? H2H_AUTO_CHUNKS : 1;
@@ -594,8 +598,12 @@ int copy_out(i7m_handle* h, double* dst, const double* src, size_t n, hipStream_
 // chunk is H2D of its rows -> its SQP -> D2H of its rows and stats, so chunk i's solve runs while
 // chunk i+1 is copied in and chunk i-1 copied out (PCIe is full duplex), instead of copy-in,
 // solve, copy-out back to back.  Ordered after earlier work on h->stream; synchronous.
+int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
+                        int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch);
+
 int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals, int goal_stride,
                       double* xu_out, i7m_problem_stats* stats, int nch) {
+  if (h->h2h_pipe) return solve_h2h_pipelined(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch);
   const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
   int rc;
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
@@ -620,6 +628,69 @@ int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* x
     HIPCHK(hipEventRecord(h->ev_done[c], h->cs[c]));
     HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[c], 0));
   }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+// The chunks as a three-stage pipeline: copies in on cs[0], the solves one after another on the
+// handle's stream, copies out on cs[1]; chunk i's solve waits only for its own copy-in, its
+// copy-out only for its solve.  Issued in the order in(0) solve(0) [in(i) solve(i) out(i-1)]...
+// out(n-1): with pinned host memory every call returns at once and the three queues overlap; with
+// pageable memory (whose copies block the calling thread until done) the host still copies chunk
+// i in, and chunk i-1 out, while the device solves the chunk before.  The alternating two-stream
+// layout above issued all copy-ins at once: they shared the link and finished together, then the
+// solves ran, then the copy-outs — no overlap.
+int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
+                        int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch) {
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  while ((int)h->ev_in.size() < nch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return fail(I7M_EHIP, "chunk event creation failed");
+    }
+    h->ev_in.push_back(a);
+    h->ev_cmp.push_back(b);
+  }
+  int rc;
+  HIPCHK(hipEventRecord(h->ev_order, h->stream));
+  for (int c = 0; c < 2; ++c) HIPCHK(hipStreamWaitEvent(h->cs[c], h->ev_order, 0));
+  auto lo_of = [&](int i) { return (long)B * i / nch; };
+  auto in = [&](int i) -> int {
+    const long lo = lo_of(i), n = lo_of(i + 1) - lo;
+    if ((rc = copy_in(h, h->d_xu + lo * T, xu_in + lo * T, n * T, h->cs[0]))) return rc;
+    if ((rc = copy_in(h, h->d_xs + lo * 12, xcur + lo * 12, (size_t)n * 12, h->cs[0]))) return rc;
+    if ((rc = copy_in(h, h->d_goal + lo * N * goal_stride, goals + lo * N * goal_stride, n * N * goal_stride, h->cs[0])))
+      return rc;
+    HIPCHK(hipEventRecord(h->ev_in[i], h->cs[0]));
+    return I7M_OK;
+  };
+  auto solve = [&](int i) -> int {
+    const long lo = lo_of(i), n = lo_of(i + 1) - lo;
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_in[i], 0));
+    double* dxu = h->d_xu + lo * T;
+    if ((rc = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
+                      h->d_stats + lo, lo, h->stream)))
+      return rc;
+    HIPCHK(hipEventRecord(h->ev_cmp[i], h->stream));
+    return I7M_OK;
+  };
+  auto out = [&](int i) -> int {
+    const long lo = lo_of(i), n = lo_of(i + 1) - lo;
+    HIPCHK(hipStreamWaitEvent(h->cs[1], h->ev_cmp[i], 0));
+    if ((rc = copy_out(h, xu_out + lo * T, h->d_xu + lo * T, n * T, h->cs[1]))) return rc;
+    if (stats)
+      HIPCHK(hipMemcpyAsync(stats + lo, h->d_stats + lo, sizeof(ProblemStats) * (size_t)n, hipMemcpyDeviceToHost,
+                            h->cs[1]));
+    return I7M_OK;
+  };
+  if ((rc = in(0)) || (rc = solve(0))) return rc;
+  for (int i = 1; i < nch; ++i)
+    if ((rc = in(i)) || (rc = solve(i)) || (rc = out(i - 1))) return rc;
+  if ((rc = out(nch - 1))) return rc;
+  HIPCHK(hipEventRecord(h->ev_done[1], h->cs[1]));
+  HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[1], 0));
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
 }
@@ -733,6 +804,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   }
   h->h2h_chunks = cfg->h2h_chunks;
   if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
+  if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
@@ -797,6 +869,8 @@ void i7m_destroy(i7m_handle* h) {
     (void)hipEventDestroy(t.b);
   }
   for (auto e : h->pool) (void)hipEventDestroy(e);
+  for (auto e : h->ev_in) (void)hipEventDestroy(e);
+  for (auto e : h->ev_cmp) (void)hipEventDestroy(e);
   drop_graphs(h);
   for (int c = 0; c < 2; ++c) {
     if (h->cs[c]) {

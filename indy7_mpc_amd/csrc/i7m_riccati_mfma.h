@@ -61,9 +61,13 @@ enum : int {
 // fp64 MFMA and fp64 VALU share one rate, and the 4x4x4_4b form retires FMAs at the 16x16x4 rate
 // (tools/probes/fp64_pipes.hip), so an MFMA costs its padded size: H's two 16x16x4 steps (128
 // cycles) did 216 useful FMAs of 2048, W1 = V B~ and G~ 23 % each.  As blocks: W (2 instructions),
-// H (2), G~ (4) = 128 cycles for what took 384.  Different summation grouping than the 16x16
-// form, so the two builds differ by rounding (both within the parity tolerances); every variant
-// (one wave, two waves, k_sqp_fused) uses the same one, so they stay bit-identical to each other.
+// H (2), G~ (4) = 128 cycles for what took 384.  Bit-identical to the 16x16 form: both MFMAs
+// accumulate their k-steps as an fma chain in k order and the padding adds exact zeros
+// (tools/lib_diff.py, -DI7M_RIC_44=0 against the default: 0 of 4096 config-3 problems, 0 of 256
+// config-4 problems and none of the 500 closed-loop steps differ in any bit).  The two-wave
+// kernel (B <= 128) keeps the 16x16 forms: there G~ feeds wave 0's elimination straight from
+// the accumulators, and the 4x4 blocks would put an LDS round trip on that chain (+2 us per launch
+// at B <= 64).
 #ifndef I7M_RIC_44
 #define I7M_RIC_44 1
 #endif
@@ -149,6 +153,12 @@ __device__ __forceinline__ Ric44Maps ric44_maps(const int l) {
   M.w0S = pk16((lq >= 2 && lr < 13) ? MO_W0V + 13 * (lq - 2) + lr : sink, (lr < 13) ? MO_W0V + 13 * (lq + 2) + lr : sink);
   return M;
 }
+// Laundered in the box body only (k_ipm_fused: 69 -> 24 VGPRs spilled).  The plain QP has the
+// registers for the hoisted unpacked maps (122 VGPRs), and unpacking at every use cost it ~6 %
+// (k_riccati_mfma 254 -> 270 us at B = 4096, N = 64); I7M_RIC44_LAUNDER_ALL=1 launders there too (A/B).
+#ifndef I7M_RIC44_LAUNDER_ALL
+#define I7M_RIC44_LAUNDER_ALL 0
+#endif
 __device__ __forceinline__ void ric44_launder(Ric44Maps& M) {
   asm volatile("" : "+v"(M.wAB[0]), "+v"(M.wAB[1]), "+v"(M.hAB[0]), "+v"(M.hAB[1]), "+v"(M.hDR), "+v"(M.wDhR2),
                "+v"(M.gA[0]), "+v"(M.gA[1]), "+v"(M.gB), "+v"(M.gD), "+v"(M.gN), "+v"(M.gN2), "+v"(M.oGB), "+v"(M.vvS),
@@ -502,8 +512,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   }
 
   // the small products on 4x4x4 blocks (I7M_RIC_44), the box body too (its Sigma_u / h_u join
-  // the C inputs); not the diagnostic LDS-exchange elimination
-  constexpr bool S44 = I7M_RIC_44 && !(ABL & 4);
+  // the C inputs); not the two-wave kernel (see I7M_RIC_44) nor the diagnostic LDS-exchange elimination
+  constexpr bool S44 = I7M_RIC_44 && !(ABL & 4) && !W2;
   Ric44Maps M44 = ric44_maps<BOX>(l);
   constexpr int SE = BOX ? 176 : 140;  // stash length
   // Branch-free lane-conditional stores (lanes with nothing to store write a per-lane sink slot,
@@ -563,7 +573,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     return (long long)__builtin_amdgcn_s_memtime();
   };
   for (int k = N - 2; k >= 0; --k) {
-    if constexpr (S44) ric44_launder(M44);
+    if constexpr (S44 && (BOX || I7M_RIC44_LAUNDER_ALL)) ric44_launder(M44);
     if constexpr (W2) {
       lds_sync();  // every wave is done with the previous stage's LDS
       if (w == 0) {

@@ -1,5 +1,5 @@
-"""A/B of the host-to-host solve (i7m_solve: numpy in, numpy out) split into chunks on two
-streams (i7m_config.h2h_chunks) at config 3 (B = 4096, N = 32): median of 20 timed calls after 3
+"""A/B of the host-to-host solve (i7m_solve: numpy in, numpy out) split into chunks
+(i7m_config.h2h_chunks; I7M_H2H_PIPE=0 for the alternating two-stream layout instead of the pipeline) at config 3 (B = 4096, N = 32): median of 20 timed calls after 3
 warm-up calls per chunk count (BASELINE.md §4's procedure), each output checked bit for bit
 against the one-piece solve.  Prints one JSON line per setting.
 
@@ -59,7 +59,7 @@ def main():
             ref = (out.copy(), st.copy())
         same = bool(np.array_equal(out, ref[0]) and np.array_equal(st, ref[1]))
         med = statistics.median(ts)
-        print(json.dumps({"h2h_chunks": nch, "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
+        print(json.dumps({"h2h_chunks": nch, "pipe": os.environ.get("I7M_H2H_PIPE", "1"), "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
                           "host_to_host_solves_per_s": a.batch / med, "min_ms": 1e3 * min(ts),
                           "bit_identical_to_first": same}), flush=True)
         h.close()
