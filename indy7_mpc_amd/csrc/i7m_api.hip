@@ -129,10 +129,14 @@ struct i7m_handle {
   int h2h_chunks = 0;
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   hipStream_t cs[2] = {nullptr, nullptr};
+  hipStream_t cs2 = nullptr;  // h2h_pipe == 2: the second solve stream (created on first use)
   hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
-  // pipelined host-to-host chunks (h2h_pipe, default; I7M_H2H_PIPE=0: the two alternating streams):
-  // per chunk, copy-in done on cs[0] -> solve on the handle's stream -> copy-out on cs[1]
-  int h2h_pipe = 1;
+  // pipelined host-to-host chunks (h2h_pipe 1 / 2; I7M_H2H_PIPE=0: the first cut's two alternating
+  // streams): per chunk, copy-in on cs[0] -> solve -> copy-out on cs[1]
+  // 2 (default): the chunks' solves alternate over two streams, so one chunk's solve may overlap the
+  // next one's start; 1: all solves on the handle's stream (A/B)
+  int h2h_pipe = 2;
+  int h2h_taper = 1;  // I7M_H2H_TAPER=0: equal chunks (A/B)
   std::vector<hipEvent_t> ev_in, ev_cmp;
   // timing
   bool timing = false;
@@ -576,13 +580,12 @@ int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, c
   return I7M_OK;
 }
 
-// chunks of a host-to-host solve of B problems: the handle's setting, else automatic
-// (H2H_AUTO_CHUNKS from H2H_AUTO_MIN_B problems on; DESIGN.md §5 has the A/B)
-constexpr int H2H_AUTO_CHUNKS = 2;
-constexpr int H2H_AUTO_MIN_B = 2048;
+// chunks of a host-to-host solve of B problems: the handle's setting, else automatic — three
+// (tapered) from 3 072 problems, two from 2 048, one piece below (config 3: 1.42 -> 1.21 ms;
+// at B = 1 024 one piece is fastest; DESIGN.md §5 has the A/B)
 int h2h_chunks_for(const i7m_handle* h, int B) {
   if (h->h2h_chunks > 0) return h->h2h_chunks;
-  return B >= H2H_AUTO_MIN_B ? H2H_AUTO_CHUNKS : 1;
+  return B >= 3072 ? 3 : (B >= 2048 ? 2 : 1);
 }
 
 int copy_in(i7m_handle* h, double* dst, const double* src, size_t n, hipStream_t s = nullptr) {
@@ -632,8 +635,9 @@ int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* x
   return I7M_OK;
 }
 
-// The chunks as a three-stage pipeline: copies in on cs[0], the solves one after another on the
-// handle's stream, copies out on cs[1]; chunk i's solve waits only for its own copy-in, its
+// The chunks as a three-stage pipeline: copies in on cs[0], the solves on the handle's stream
+// (h2h_pipe 1) or alternating between it and cs2 (2, default: a chunk's solve can start while the
+// previous one drains), copies out on cs[1]; chunk i's solve waits only for its own copy-in, its
 // copy-out only for its solve.  Issued in the order in(0) solve(0) [in(i) solve(i) out(i-1)]...
 // out(n-1): with pinned host memory every call returns at once and the three queues overlap; with
 // pageable memory (whose copies block the calling thread until done) the host still copies chunk
@@ -654,9 +658,19 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
     h->ev_cmp.push_back(b);
   }
   int rc;
+  if (h->h2h_pipe == 2 && !h->cs2) HIPCHK(hipStreamCreateWithFlags(&h->cs2, hipStreamNonBlocking));
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
   for (int c = 0; c < 2; ++c) HIPCHK(hipStreamWaitEvent(h->cs[c], h->ev_order, 0));
-  auto lo_of = [&](int i) { return (long)B * i / nch; };
+  if (h->h2h_pipe == 2) HIPCHK(hipStreamWaitEvent(h->cs2, h->ev_order, 0));
+  auto sstream = [&](int i) { return (h->h2h_pipe == 2 && (i & 1)) ? h->cs2 : h->stream; };
+  // taper (default; I7M_H2H_TAPER=0 for equal chunks): the first and the last chunk half the size
+  // of the others, so the copy-in before the first solve and the copy-out after the last are short
+  auto lo_of = [&](int i) -> long {
+    if (!h->h2h_taper || nch < 3) return (long)B * i / nch;
+    if (i == 0) return 0;
+    if (i == nch) return B;
+    return (long)((double)B * (2 * i - 1) / (2.0 * (nch - 1)));
+  };
   auto in = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
     if ((rc = copy_in(h, h->d_xu + lo * T, xu_in + lo * T, n * T, h->cs[0]))) return rc;
@@ -668,19 +682,20 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
   };
   auto solve = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
-    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_in[i], 0));
+    const hipStream_t ss = sstream(i);
+    HIPCHK(hipStreamWaitEvent(ss, h->ev_in[i], 0));
     double* dxu = h->d_xu + lo * T;
-    if ((rc = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
-                      h->d_stats + lo, lo, h->stream)))
+    if (n > 0 && (rc = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
+                               h->d_stats + lo, lo, ss)))
       return rc;
-    HIPCHK(hipEventRecord(h->ev_cmp[i], h->stream));
+    HIPCHK(hipEventRecord(h->ev_cmp[i], ss));
     return I7M_OK;
   };
   auto out = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
     HIPCHK(hipStreamWaitEvent(h->cs[1], h->ev_cmp[i], 0));
     if ((rc = copy_out(h, xu_out + lo * T, h->d_xu + lo * T, n * T, h->cs[1]))) return rc;
-    if (stats)
+    if (stats && n > 0)
       HIPCHK(hipMemcpyAsync(stats + lo, h->d_stats + lo, sizeof(ProblemStats) * (size_t)n, hipMemcpyDeviceToHost,
                             h->cs[1]));
     return I7M_OK;
@@ -804,7 +819,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   }
   h->h2h_chunks = cfg->h2h_chunks;
   if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
-  if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::atoi(e) != 0;
+  if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("I7M_H2H_TAPER")) h->h2h_taper = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
@@ -872,6 +888,10 @@ void i7m_destroy(i7m_handle* h) {
   for (auto e : h->ev_in) (void)hipEventDestroy(e);
   for (auto e : h->ev_cmp) (void)hipEventDestroy(e);
   drop_graphs(h);
+  if (h->cs2) {
+    (void)hipStreamSynchronize(h->cs2);
+    (void)hipStreamDestroy(h->cs2);
+  }
   for (int c = 0; c < 2; ++c) {
     if (h->cs[c]) {
       (void)hipStreamSynchronize(h->cs[c]);

@@ -59,7 +59,7 @@ def main():
             ref = (out.copy(), st.copy())
         same = bool(np.array_equal(out, ref[0]) and np.array_equal(st, ref[1]))
         med = statistics.median(ts)
-        print(json.dumps({"h2h_chunks": nch, "pipe": os.environ.get("I7M_H2H_PIPE", "1"), "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
+        print(json.dumps({"h2h_chunks": nch, "pipe": os.environ.get("I7M_H2H_PIPE", "2"), "taper": os.environ.get("I7M_H2H_TAPER", "1"), "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
                           "host_to_host_solves_per_s": a.batch / med, "min_ms": 1e3 * min(ts),
                           "bit_identical_to_first": same}), flush=True)
         h.close()
