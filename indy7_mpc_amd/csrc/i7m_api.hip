@@ -8,11 +8,13 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/indy7_mpc.h"
@@ -129,12 +131,13 @@ struct i7m_handle {
   int h2h_chunks = 0;
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   hipStream_t cs[2] = {nullptr, nullptr};
-  hipStream_t cs2 = nullptr;  // h2h_pipe == 2: the second solve stream (created on first use)
+  hipStream_t cs2 = nullptr;  // h2h_pipe >= 2: the second solve stream (created on first use)
   hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
   // pipelined host-to-host chunks (h2h_pipe 1 / 2; I7M_H2H_PIPE=0: the first cut's two alternating
   // streams): per chunk, copy-in on cs[0] -> solve -> copy-out on cs[1]
   // 2 (default): the chunks' solves alternate over two streams, so one chunk's solve may overlap the
-  // next one's start; 1: all solves on the handle's stream (A/B)
+  // next one's start; 1: all solves on the handle's stream (A/B); 3: as 2, with the
+  // copies out issued by a second host thread (pageable copies block the issuing thread)
   int h2h_pipe = 2;
   int h2h_taper = 1;  // I7M_H2H_TAPER=0: equal chunks (A/B)
   std::vector<hipEvent_t> ev_in, ev_cmp;
@@ -658,11 +661,11 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
     h->ev_cmp.push_back(b);
   }
   int rc;
-  if (h->h2h_pipe == 2 && !h->cs2) HIPCHK(hipStreamCreateWithFlags(&h->cs2, hipStreamNonBlocking));
+  if (h->h2h_pipe >= 2 && !h->cs2) HIPCHK(hipStreamCreateWithFlags(&h->cs2, hipStreamNonBlocking));
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
   for (int c = 0; c < 2; ++c) HIPCHK(hipStreamWaitEvent(h->cs[c], h->ev_order, 0));
-  if (h->h2h_pipe == 2) HIPCHK(hipStreamWaitEvent(h->cs2, h->ev_order, 0));
-  auto sstream = [&](int i) { return (h->h2h_pipe == 2 && (i & 1)) ? h->cs2 : h->stream; };
+  if (h->h2h_pipe >= 2) HIPCHK(hipStreamWaitEvent(h->cs2, h->ev_order, 0));
+  auto sstream = [&](int i) { return (h->h2h_pipe >= 2 && (i & 1)) ? h->cs2 : h->stream; };
   // taper (default; I7M_H2H_TAPER=0 for equal chunks): the first and the last chunk half the size
   // of the others, so the copy-in before the first solve and the copy-out after the last are short
   auto lo_of = [&](int i) -> long {
@@ -671,12 +674,14 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
     if (i == nch) return B;
     return (long)((double)B * (2 * i - 1) / (2.0 * (nch - 1)));
   };
+  // (each stage keeps its status in a local: with h2h_pipe 3 out() runs on another thread)
   auto in = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
-    if ((rc = copy_in(h, h->d_xu + lo * T, xu_in + lo * T, n * T, h->cs[0]))) return rc;
-    if ((rc = copy_in(h, h->d_xs + lo * 12, xcur + lo * 12, (size_t)n * 12, h->cs[0]))) return rc;
-    if ((rc = copy_in(h, h->d_goal + lo * N * goal_stride, goals + lo * N * goal_stride, n * N * goal_stride, h->cs[0])))
-      return rc;
+    int r;
+    if ((r = copy_in(h, h->d_xu + lo * T, xu_in + lo * T, n * T, h->cs[0]))) return r;
+    if ((r = copy_in(h, h->d_xs + lo * 12, xcur + lo * 12, (size_t)n * 12, h->cs[0]))) return r;
+    if ((r = copy_in(h, h->d_goal + lo * N * goal_stride, goals + lo * N * goal_stride, n * N * goal_stride, h->cs[0])))
+      return r;
     HIPCHK(hipEventRecord(h->ev_in[i], h->cs[0]));
     return I7M_OK;
   };
@@ -685,25 +690,66 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
     const hipStream_t ss = sstream(i);
     HIPCHK(hipStreamWaitEvent(ss, h->ev_in[i], 0));
     double* dxu = h->d_xu + lo * T;
-    if (n > 0 && (rc = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
-                               h->d_stats + lo, lo, ss)))
-      return rc;
+    int r;
+    if (n > 0 && (r = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
+                              h->d_stats + lo, lo, ss)))
+      return r;
     HIPCHK(hipEventRecord(h->ev_cmp[i], ss));
     return I7M_OK;
   };
   auto out = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
     HIPCHK(hipStreamWaitEvent(h->cs[1], h->ev_cmp[i], 0));
-    if ((rc = copy_out(h, xu_out + lo * T, h->d_xu + lo * T, n * T, h->cs[1]))) return rc;
+    int r;
+    if ((r = copy_out(h, xu_out + lo * T, h->d_xu + lo * T, n * T, h->cs[1]))) return r;
     if (stats && n > 0)
       HIPCHK(hipMemcpyAsync(stats + lo, h->d_stats + lo, sizeof(ProblemStats) * (size_t)n, hipMemcpyDeviceToHost,
                             h->cs[1]));
     return I7M_OK;
   };
-  if ((rc = in(0)) || (rc = solve(0))) return rc;
-  for (int i = 1; i < nch; ++i)
-    if ((rc = in(i)) || (rc = solve(i)) || (rc = out(i - 1))) return rc;
-  if ((rc = out(nch - 1))) return rc;
+  if (h->h2h_pipe == 3) {
+    // copies out on a second host thread: a pageable copy blocks the thread that issues it, so
+    // with one thread every copy-out sat between two copy-ins and the link ran one direction at a
+    // time; here the calling thread issues in(0) solve(0) in(1) solve(1) ... back to back while the
+    // helper issues out(i) as soon as solve(i) has been issued (it then blocks in the copy until
+    // the solve and the copy are done) — both directions of the link in flight together
+    std::atomic<int> issued{0};
+    int rc_out = I7M_OK;
+    std::string err_out;
+    std::thread helper([&] {
+      if (hipSetDevice(h->dev) != hipSuccess) {
+        rc_out = I7M_EHIP;
+        err_out = "hipSetDevice failed (copy-out thread)";
+        return;
+      }
+      int r = I7M_OK;
+      for (int i = 0; i < nch && r == I7M_OK; ++i) {
+        int k;
+        while ((k = issued.load(std::memory_order_acquire)) <= i) {
+          if (k < 0) return;  // the calling thread failed: nothing more to copy
+          std::this_thread::yield();
+        }
+        r = out(i);
+      }
+      if (r != I7M_OK) {
+        rc_out = r;
+        err_out = g_err;  // thread_local: hand the message to the calling thread
+      }
+    });
+    int r = I7M_OK;
+    for (int i = 0; i < nch && r == I7M_OK; ++i) {
+      if ((r = in(i)) == I7M_OK && (r = solve(i)) == I7M_OK) issued.store(i + 1, std::memory_order_release);
+    }
+    if (r != I7M_OK) issued.store(-1, std::memory_order_release);
+    helper.join();
+    if (r != I7M_OK) return r;
+    if (rc_out != I7M_OK) return fail(rc_out, err_out);
+  } else {
+    if ((rc = in(0)) || (rc = solve(0))) return rc;
+    for (int i = 1; i < nch; ++i)
+      if ((rc = in(i)) || (rc = solve(i)) || (rc = out(i - 1))) return rc;
+    if ((rc = out(nch - 1))) return rc;
+  }
   HIPCHK(hipEventRecord(h->ev_done[1], h->cs[1]));
   HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[1], 0));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -819,7 +865,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   }
   h->h2h_chunks = cfg->h2h_chunks;
   if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
-  if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::min(std::max(std::atoi(e), 0), 3);
   if (const char* e = std::getenv("I7M_H2H_TAPER")) h->h2h_taper = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));

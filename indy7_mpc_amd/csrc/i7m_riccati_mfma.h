@@ -51,9 +51,10 @@ enum : int {
   MO_VV = 610,
   MO_WV = 646,
   MO_W0V = 682,
-  MO_TOTAL = 760,
-  MO_QX = 760,   // 256  two-wave body: Qxx~ of wave 1 in the accumulator layout (64 i + lane)
-  MO_TOTAL_W2 = 1016,
+  MO_DT = 760,   // dt (A~'s q rows read as LDS operands like its v rows)
+  MO_TOTAL = 762,
+  MO_QX = 762,   // 256  two-wave body: Qxx~ of wave 1 in the accumulator layout (64 i + lane)
+  MO_TOTAL_W2 = 1018,
 };
 
 // I7M_RIC_44 (default 1): the stage's small products — H = Bu V_vv Bu + R and G~ = Bu W0_v + N~
@@ -79,6 +80,13 @@ enum : int {
 // column block) = (s & 1, (s ^ (s >> 1)) & 1): 0 (0,0), 1 (1,1), 2 (0,1), 3 (1,0).
 __device__ __forceinline__ double mfma44(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+// f64 MFMA neg modifiers (the blgp field: bit 0 negates A, bit 1 B, bit 2 C): -(a b) - c, -(a b) + c
+__device__ __forceinline__ double mfma44_nac(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 5);
+}
+__device__ __forceinline__ double mfma44_na(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1);
 }
 __device__ __forceinline__ int blk_r(int s) { return s & 1; }
 __device__ __forceinline__ int blk_c(int s) { return (s ^ (s >> 1)) & 1; }
@@ -177,7 +185,10 @@ __device__ __forceinline__ void ric44_h(const Ric44Maps& M, double* __restrict__
   h = mfma44(sh[lo16(M.hAB[1])], sh[hi16(M.hAB[1])], h);
   sh[lo16(M.hDR)] = h;
 }
-// G~ = Bu' W0_v + N~ (+ h_u) into MO_G (needs W0_v, Bu, r in LDS; one wave)
+// -G~ = -(Bu' W0_v + N~ (+ h_u)) into MO_G (needs W0_v, Bu, r in LDS; one wave).  Negated by the
+// MFMA's neg modifiers (first k-step: A and C, second: A), which negate every rounded partial sum
+// exactly: the elimination of [H | -G~] then ends at K~ = -H^-1 G~ itself (no negation pass), and
+// V~'s update takes -G~ with its B operand negated.
 template <bool BOX>
 __device__ __forceinline__ void ric44_g(const Ric44Maps& M, double* __restrict__ sh) {
   const double b0 = sh[lo16(M.gB)], b1 = sh[hi16(M.gB)];
@@ -186,16 +197,19 @@ __device__ __forceinline__ void ric44_g(const Ric44Maps& M, double* __restrict__
     g0 += sh[lo16(M.gN2)];
     g1 += sh[hi16(M.gN2)];
   }
-  g0 = mfma44(sh[lo16(M.gA[0])], b0, g0);
-  g1 = mfma44(sh[hi16(M.gA[0])], b0, g1);
-  g0 = mfma44(sh[lo16(M.gA[1])], b1, g0);
-  g1 = mfma44(sh[hi16(M.gA[1])], b1, g1);
+  g0 = mfma44_nac(sh[lo16(M.gA[0])], b0, g0);
+  g1 = mfma44_nac(sh[hi16(M.gA[0])], b0, g1);
+  g0 = mfma44_na(sh[lo16(M.gA[1])], b1, g0);
+  g1 = mfma44_na(sh[hi16(M.gA[1])], b1, g1);
   sh[lo16(M.gD)] = g0;
   sh[hi16(M.gD)] = g1;
 }
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ d4 mfma_nb(double a, double b, d4 c) {  // a (-b) + c
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 2);
 }
 
 // v from lane `src` (wave-uniform src) into every lane, via two v_readlane_b32 (SGPR broadcast).
@@ -333,15 +347,21 @@ __device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& 
     return LINb + (e - KBUF_STRIDE);
   };
   int fs0, fs1, fs2;
+  // running pointers to the next stage to prefetch (nf), stepped one stage per load and held at
+  // the last stage (the loads past it are dummies): no per-load stride multiply
   const double* fb0 = fbase(l, fs0);
   const double* fb1 = fbase(l + 64, fs1);
   const double* fb2 = fbase(l + 128, fs2);
+  int nf = 0;
   // slot position of stage element e
+  // lane m < 6: K~ row m (K 0..11, kff 12); lane 6 + i: Aq row i (0..5), Av row i (6..11), c_v[i]
+  // (12), Bu row i (13..18) — the same places for x and the constant, so one 12-term chain gives
+  // u on lanes 0..5 and A x + c on lanes 6..11
   auto fpos = [](int e) -> int {
     if (e < 78) return FB * (e / 13) + e % 13;
-    if (e < 84) return FB * (6 + e - 78);
+    if (e < 84) return FB * (6 + e - 78) + 12;
     const int t = e - 84, blk = t / 36, w = t % 36;
-    return FB * (6 + w / 6) + 1 + 6 * blk + w % 6;
+    return FB * (6 + w / 6) + (blk < 2 ? 6 * blk : 13) + w % 6;
   };
   const int w0 = fpos(l), w1 = fpos(l + 64), w2 = fpos(l + 128);
   double* myb = sh + FB * (l < 12 ? l : 12);
@@ -352,10 +372,16 @@ __device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& 
   // stage wait for the loads it had just issued.
   constexpr int FD = I7M_RIC_FD;
   double f[FD][3];
-  auto fload = [&](double* f, int kk) {
-    f[0] = fb0[(long)kk * fs0];
-    f[1] = fb1[(long)kk * fs1];
-    f[2] = fb2[(long)kk * fs2];
+  auto fload = [&](double* f) {
+    f[0] = *fb0;
+    f[1] = *fb1;
+    f[2] = *fb2;
+    if (nf < N - 2) {  // wave-uniform
+      ++nf;
+      fb0 += fs0;
+      fb1 += fs1;
+      fb2 += fs2;
+    }
   };
   double xreg = (l < 12) ? xs[(long)b * 12 + l] : 0.0;
   if (l < 12) S[l] = xreg;
@@ -363,20 +389,20 @@ __device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& 
   // x_0 load into the loop and every stage waits for the loads it has just issued
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
-  for (int d = 0; d < FD; ++d) fload(f[d], d < N - 1 ? d : 0);
+  for (int d = 0; d < FD; ++d) fload(f[d]);
   auto stage = [&](const int k, double* fk) {
     if (PRIO && I7M_RIC_PRIO_S != 0) set_prio(ric_prio_fwd(k, N));
     double r[19];
     if (ABL & 128) {
 #pragma unroll
       for (int j = 0; j < 19; ++j) r[j] = fk[j % 3] * (j + 1);
-      fload(fk, (k + FD < N - 1) ? k + FD : k);
+      fload(fk);
     } else {
     wave_sync();
     sh[w0] = fk[0];
     sh[w1] = fk[1];
     sh[w2] = fk[2];
-    fload(fk, (k + FD < N - 1) ? k + FD : k);
+    fload(fk);
     wave_sync();
 #pragma unroll
     for (int j = 0; j < 19; ++j) r[j] = myb[j];
@@ -389,7 +415,8 @@ __device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& 
 #pragma unroll
       for (int j = 0; j < 12; ++j) X[j] = readlane_f64(xreg, j);
     }
-    // u (lanes 0..5): two partial sums to halve the dependency chain
+    // u = K~ [x; 1] on lanes 0..5 and c_v + Aq x_q + Av x_v on lanes 6..11 by the same chain
+    // (two partial sums to halve its length)
     double ua = r[12], ub = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) { ua += r[j] * X[j]; ub += r[6 + j] * X[6 + j]; }
@@ -402,16 +429,12 @@ __device__ __forceinline__ void riccati_rollout(const int b, const SolveParams& 
 #pragma unroll
       for (int j = 0; j < 6; ++j) U[j] = readlane_f64(ureg, j);
     }
-    double va = r[0], vb = 0.0, vc = 0.0;
+    double vc = 0.0;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      va += r[1 + j] * X[j];
-      vb += r[7 + j] * X[6 + j];
-      vc += r[13 + j] * ((ABL & 64) ? X[j] : U[j]);
-    }
+    for (int j = 0; j < 6; ++j) vc += r[13 + j] * ((ABL & 64) ? X[j] : U[j]);
     // q lanes: q + dt v, v_l = x_{6+l} from lane l + 6 (DPP row shift, same 16-lane row)
     const double vq = row_shl6_f64(xreg);
-    const double nx = (l < 6) ? xreg + dt * vq : (va + vb) + vc;
+    const double nx = (l < 6) ? xreg + dt * vq : ureg + vc;
     xreg = nx;
     if (!(ABL & 32) && (!(ABL & 256) || k == N - 2) && l < 12) S[18 * (k + 1) + l] = nx;
   };
@@ -455,23 +478,23 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   double* KB = kbuf + (long)b * (N - 1) * KBUF_STRIDE;
 
   // ---- per-lane operand maps (fixed for the whole kernel)
-  // A~[4s+lq][lr] = sh[offA[s]] + cA[s]
+  // A~[4s+lq][lr] = sh[offA[s]] for k-steps s = 1, 2 (the q rows' 1 and dt from the MO_ONE / MO_DT
+  // slots, so no per-stage add of a constant); k-step 0 is all q rows, the stage-invariant cA0.
+  // (k-step 3 — row 12 — is the select on W0 / Qxx below, not an MFMA.)
   int offA[4];
-  double cA[4];
+  const double cA0 = (lr == lq) ? 1.0 : (lr == lq + 6 ? dt : 0.0);
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int k = 4 * s + lq, c = lr;
     offA[s] = MO_ZERO;
-    cA[s] = 0.0;
     if (k < 6) {
-      cA[s] = (c == k) ? 1.0 : (c == k + 6 ? dt : 0.0);
+      offA[s] = (c == k) ? MO_ONE : (c == k + 6 ? MO_DT : MO_ZERO);
     } else if (k < 12) {
       const int i = k - 6;
       offA[s] = c < 6 ? MO_AQ + 6 * i + c : (c < 12 ? MO_AV + 6 * i + (c - 6) : (c == 12 ? MO_CV + i : MO_ZERO));
-    } else if (k == 12) {
-      cA[s] = (c == 12) ? 1.0 : 0.0;
     }
   }
+  auto opA = [&](int s) -> double { return s == 0 ? cA0 : sh[offA[s]]; };
   // B~[4s+lq][lr] for s = 1, 2
   int offB[2];
 #pragma unroll
@@ -503,6 +526,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     oR2[i] = (BOX && r == c && r < 6) ? MO_SIG + 12 + r : MO_ZERO;
     oN2[i] = (BOX && c == 12 && r < 6) ? MO_HB + 12 + r : MO_ZERO;
   }
+  const double m12 = (lr == 12) ? 1.0 : 0.0, mlq0 = (lq == 0) ? 1.0 : 0.0;
   // K~[4s+lq][lr] for s = 0, 1
   int oK[2];
 #pragma unroll
@@ -535,12 +559,22 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   };
   const int e2 = (l + 128 < SE) ? l + 128 : SE - 1;
   int st0, st1, st2;
-  const double* sb0 = base_of(l, st0);
-  const double* sb1 = base_of(l + 64, st1);
-  const double* sb2 = base_of(e2, st2);
+  // running pointers, stepped back one stage per stage: a per-lane stride times the stage index
+  // cost two v_mad_u64_u32 (quarter rate) and their moves per element and stage
+  const double* sb0 = base_of(l, st0) + (long)(N - 2) * st0;
+  const double* sb1 = base_of(l + 64, st1) + (long)(N - 2) * st1;
+  const double* sb2 = base_of(e2, st2) + (long)(N - 2) * st2;
   // (the first stage's stash is requested before the terminal record, so its latency overlaps
   // the record's own loads)
-  double p0 = sb0[(long)(N - 2) * st0], p1 = sb1[(long)(N - 2) * st1], p2 = sb2[(long)(N - 2) * st2];
+  double p0 = *sb0, p1 = *sb1, p2 = *sb2;
+  auto stash_next = [&]() {
+    sb0 -= st0;
+    sb1 -= st1;
+    sb2 -= st2;
+    p0 = *sb0;
+    p1 = *sb1;
+    p2 = *sb2;
+  };
 
   // ---- terminal cost-to-go V~ = Q~_{N-1}: the terminal knot's record from cost and XU
   {
@@ -555,6 +589,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     } else if (l == 13) {
       sh[MO_ZERO] = 0.0;
       sh[MO_ONE] = 1.0;
+      sh[MO_DT] = dt;
     }
     if (BOX && l < 12) {
       sh[MO_SIG + l] = bsig[(long)b * P.T + 18 * (N - 1) + l];
@@ -586,10 +621,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         }
       }
       lds_sync();
-      if (w == 0 && k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
-      double bA[4], bB[2];
+      if (w == 0 && k > 0) stash_next();
+      double bA[3], bB[2];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
+      for (int s = 0; s < 3; ++s) bA[s] = opA(s);
       bB[0] = sh[offB[0]];
       bB[1] = sh[offB[1]];
       d4 W0, Z00, Z10;
@@ -706,10 +741,10 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[hi16(M44.vvS)] = V[2];
     }
     wave_sync();
-    if (k > 0) { p0 = sb0[(long)(k - 1) * st0]; p1 = sb1[(long)(k - 1) * st1]; p2 = sb2[(long)(k - 1) * st2]; }
-    double bA[4], bB[2];
+    if (k > 0) stash_next();
+    double bA[3], bB[2];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) bA[s] = sh[offA[s]] + cA[s];
+    for (int s = 0; s < 3; ++s) bA[s] = opA(s);
     d4 Qi, Ri, Ni;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -726,10 +761,11 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     }
     // W0 = V A~ ; Qxx = A~' W0 + Q~.  Rows 12..15 of A~ are e_12' and 0: their k-step is a
     // select (W0[:,12] += V[:,12], Qxx[12,:] += W0[12,:]) instead of an MFMA.
-    if (ABL & 512) ta = tstamp(bA[0] + bA[1] + bA[2] + bA[3] + bB[0] + bB[1] + Qi[0] + Ri[0] + Ni[0]);
+    if (ABL & 512) ta = tstamp(bA[0] + bA[1] + bA[2] + bB[0] + bB[1] + Qi[0] + Ri[0] + Ni[0]);
     d4 W0;
+    // (lr == 12 ? V : +0) as one fma per register instead of two 32-bit selects
 #pragma unroll
-    for (int i = 0; i < 4; ++i) W0[i] = (lr == 12) ? V[i] : 0.0;
+    for (int i = 0; i < 4; ++i) W0[i] = fma(V[i], m12, 0.0);
 #pragma unroll
     for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
     if (ABL & 512) tb = tstamp(W0[0] + W0[1] + W0[2] + W0[3]);
@@ -741,7 +777,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[lo16(M44.w0S)] = W0[1];
       sh[hi16(M44.w0S)] = W0[2];
       ric44_h<BOX>(M44, sh);
-      if (lq == 0) Z00[3] += W0[3];
+      Z00[3] = fma(W0[3], mlq0, Z00[3]);  // row 12's k-step: + W0[12][:] on the lanes lq == 0
 #pragma unroll
       for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
       ric44_g<BOX>(M44, sh);
@@ -755,7 +791,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     W1 = mfma(V[2], bB[1], W1);
     Z11 = mfma(bB[0], W1[1], Ri);
     Z11 = mfma(bB[1], W1[2], Z11);
-    if (ABL & 512) tm1 = tstamp(bA[0] + bA[1] + bA[2] + bA[3] + Qi[0] + Ri[0] + Ni[0]);
+    if (ABL & 512) tm1 = tstamp(bA[0] + bA[1] + bA[2] + Qi[0] + Ri[0] + Ni[0]);
     Z10 = mfma(bB[0], W0[1], Ni);
     Z10 = mfma(bB[1], W0[2], Z10);
     if (ABL & 512) tm2 = tstamp(Z10[0] + Z10[1] + Z11[0] + Z11[1]);
@@ -866,8 +902,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         const bool kw = cc_own >= 6 && cc_own < 19;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-          if (BF) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = -E[i];
-          else if (kw) sh[MO_KT + 13 * i + (cc_own - 6)] = -E[i];
+          const double ki = S44 ? E[i] : -E[i];  // S44: the G~ columns were eliminated from -G~
+          if (BF) sh[kw ? MO_KT + 13 * i + (cc_own - 6) : MO_DUMMY + l] = ki;
+          else if (kw) sh[MO_KT + 13 * i + (cc_own - 6)] = ki;
         }
       }
       if (HINV && cc_own >= 19 && cc_own < 25) {
@@ -877,8 +914,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       wave_sync();
       if (ABL & 512) tm3 = tstamp(E[0]);
-      V = mfma(sh[oK[0]], Z10[0], Z00);
-      V = mfma(sh[oK[1]], Z10[1], V);
+      if constexpr (S44) {  // Z10 holds -G~ (ric44_g)
+        V = mfma_nb(sh[oK[0]], Z10[0], Z00);
+        V = mfma_nb(sh[oK[1]], Z10[1], V);
+      } else {
+        V = mfma(sh[oK[0]], Z10[0], Z00);
+        V = mfma(sh[oK[1]], Z10[1], V);
+      }
       if (ABL & 512) {
         const long long tm4 = tstamp(V[0] + V[1] + V[2] + V[3]);
         if (b == 0 && l == 0) {

@@ -297,18 +297,18 @@ def test_fused_device_solve_out_of_place(lib, model):
         np.testing.assert_array_equal(st["alphas"], st_ref["alphas"])
 
 
-@pytest.mark.parametrize("layout", ["pipeline", "taper", "two_solve_streams", "alternating"])
+@pytest.mark.parametrize("layout", ["pipeline", "taper", "two_solve_streams", "alternating", "copy_out_thread"])
 @pytest.mark.parametrize("chunks", [2, 3, 7])
 def test_chunked_host_to_host_solve_bit_identical(lib, model, monkeypatch, chunks, layout):
     """i7m_solve split into chunks (h2h_chunks, copies overlapping solves) gives the one-piece
     solve's XU and stats bit for bit, also for chunks that do not divide B: the default pipeline
     (copy-in / solve / copy-out streams), its tapered chunk sizes (I7M_H2H_TAPER), the solves on
-    two alternating streams (I7M_H2H_PIPE=2) and the alternating two-stream layout
-    (I7M_H2H_PIPE=0)."""
+    two alternating streams (I7M_H2H_PIPE=2), the copies out from a second host thread
+    (I7M_H2H_PIPE=3, tapered) and the alternating two-stream layout (I7M_H2H_PIPE=0)."""
     from oracle.osqp_ref import synthetic_batch
 
-    monkeypatch.setenv("I7M_H2H_PIPE", {"alternating": "0", "two_solve_streams": "2"}.get(layout, "1"))
-    monkeypatch.setenv("I7M_H2H_TAPER", "1" if layout == "taper" else "0")
+    monkeypatch.setenv("I7M_H2H_PIPE", {"alternating": "0", "two_solve_streams": "2", "copy_out_thread": "3"}.get(layout, "1"))
+    monkeypatch.setenv("I7M_H2H_TAPER", "1" if layout in ("taper", "copy_out_thread") else "0")
     B, N = 300, 32
     xcur, goals, XU = synthetic_batch(B, N, seed=71)
     h1 = lib.Handle(model, N=N, max_batch=B, h2h_chunks=1)
