@@ -72,6 +72,12 @@ enum : int {
 #ifndef I7M_RIC_44
 #define I7M_RIC_44 1
 #endif
+// I7M_QXX_K0_VALU (default 1): Qxx's k-step over A~'s q rows 0..3 as VALU adds / fmas and a lane-half
+// swap instead of a 16x16x4 MFMA (one-wave body); bit-identical (one nonzero term per entry).
+#ifndef I7M_QXX_K0_VALU
+#define I7M_QXX_K0_VALU 1
+#endif
+
 
 // v_mfma_f64_4x4x4_4b: four independent 4 x 4 x 4 blocks.  Lane layouts (gfx950, probed by
 // tools/probes/mfma_f64_4x4_layout.hip): A lane 16k + 4s + i = A_s[i][k], B lane 16k + 4s + j =
@@ -527,6 +533,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     oN2[i] = (BOX && c == 12 && r < 6) ? MO_HB + 12 + r : MO_ZERO;
   }
   const double m12 = (lr == 12) ? 1.0 : 0.0, mlq0 = (lq == 0) ? 1.0 : 0.0;
+  const double mdt_hi = (lq >= 2) ? dt : 0.0, mdt_lo = (lq < 2) ? dt : 0.0;
   // K~[4s+lq][lr] for s = 0, 1
   int oK[2];
 #pragma unroll
@@ -749,7 +756,9 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       // (x + 0.0 is not folded for doubles: the box shifts are added only in BOX builds)
-      Qi[i] = BOX ? sh[q1[i]] * sh[q2[i]] + sh[oS[i]] : sh[q1[i]] * sh[q2[i]];
+      // (rows >= 8 — registers 2, 3 — hold no rank-1 entries: their second factor is 1 or the
+      // first is 0, so the product is the first factor itself)
+      Qi[i] = BOX ? (i < 2 ? sh[q1[i]] * sh[q2[i]] : sh[q1[i]]) + sh[oS[i]] : (i < 2 ? sh[q1[i]] * sh[q2[i]] : sh[q1[i]]);
     if constexpr (!S44) {
       bB[0] = sh[offB[0]];
       bB[1] = sh[offB[1]];
@@ -778,8 +787,32 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[hi16(M44.w0S)] = W0[2];
       ric44_h<BOX>(M44, sh);
       Z00[3] = fma(W0[3], mlq0, Z00[3]);  // row 12's k-step: + W0[12][:] on the lanes lq == 0
+      if constexpr (I7M_QXX_K0_VALU) {
+        // k-step 0 (A~'s q rows 0..3: 1 at (k, k), dt at (k, k + 6)) on the VALU: rows 0..3 of Qxx
+        // gain W0's rows 0..3 (same lanes), rows 6..9 dt times them (the other half of the wave:
+        // one v_permlane32_swap per dword).  One nonzero term per entry, rounded as the MFMA's
+        // k-step rounds it (bit-identical).
+        // Q~'s rank-1 products stay rounded on their own, as the MFMA's C input (otherwise the
+        // compiler contracts them into the adds below)
+        asm volatile("" : "+v"(Z00[0]), "+v"(Z00[1]));
+        Z00[0] = Z00[0] + W0[0];
+        const long long wb = __double_as_longlong(W0[0]);
+        const auto slo = __builtin_amdgcn_permlane32_swap((unsigned)wb, (unsigned)wb, false, false);
+        const auto shi = __builtin_amdgcn_permlane32_swap((unsigned)(wb >> 32), (unsigned)(wb >> 32), false, false);
+        // lanes 32..63 of the first result: W0 from lanes 0..31 (rows 0, 1); lanes 0..31 of the
+        // second: from lanes 32..63 (rows 2, 3)
+        const double up = __longlong_as_double(((long long)shi[0] << 32) | (unsigned)slo[0]);
+        const double dn = __longlong_as_double(((long long)shi[1] << 32) | (unsigned)slo[1]);
+        // (an fma: the MFMA's k-step adds its exact product to C — measured: a separately rounded
+        // product changes 4 091 of 4 096 config-3 solves, the fma none)
+        Z00[1] = fma(up, mdt_hi, Z00[1]);  // rows 6, 7 (lq 2, 3)
+        Z00[2] = fma(dn, mdt_lo, Z00[2]);  // rows 8, 9 (lq 0, 1)
 #pragma unroll
-      for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+        for (int s = 1; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+      }
       ric44_g<BOX>(M44, sh);
     } else {
     if (lq == 0) Z00[3] += W0[3];
