@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session: bitwise tools/lib_diff.py of each variant in DIFFS against the reference variant
-# REF, an environment A/B (VAR over VALUES, tools/env_ab.sh), config-4 A/B of C4LIBS, then the GPU tests.
-#   REF=x DIFFS="main y" VAR=I7M_RIC_BC VALUES="7 15" C4LIBS="main z" TAG=t bash tools/diff_ab_session.sh
+# REF, the split-pipeline A/B of LIBS (tools/lin_ab.sh), an environment A/B (VAR over VALUES,
+# tools/env_ab.sh), config-4 A/B of C4LIBS, then the GPU tests.
+#   REF=x DIFFS="main y" LIBS="x main" VAR=I7M_RIC_BC VALUES="7 15" C4LIBS="main z" TAG=t bash tools/diff_ab_session.sh
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 O=gpurun_out/${TAG:-dab}; mkdir -p $O
@@ -10,6 +11,10 @@ for L in ${REF:?} ${DIFFS:-}; do
   I7M_LIB=$(lp $L) timeout -k 10 300 python tools/lib_diff.py dump $O/d_$L.npz >> $O/diff.log 2>&1 || { tail -20 $O/diff.log; exit 3; }
 done
 for L in ${DIFFS:-}; do echo "== lib_diff $REF vs $L"; python tools/lib_diff.py cmp $O/d_$REF.npz $O/d_$L.npz | tee $O/lib_diff_$L.txt; done
+if [ -n "${LIBS:-}" ]; then
+  LIBS="$LIBS" BATCHES=${BATCHES:-4096,1024,64,1} TAG=${TAG:-dab} bash tools/lin_ab.sh > $O/lin_ab.txt 2>&1 || { tail -20 $O/lin_ab.txt; exit 4; }
+  cat $O/lin_ab.txt
+fi
 if [ -n "${VAR:-}" ]; then
   VAR=$VAR VALUES="$VALUES" BATCHES=${BATCHES:-4096,2048,1024} TAG=${TAG:-dab} bash tools/env_ab.sh > $O/env_ab.txt 2>&1 || { tail -20 $O/env_ab.txt; exit 5; }
   cat $O/env_ab.txt
