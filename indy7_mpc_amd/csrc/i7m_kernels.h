@@ -12,6 +12,8 @@
 //                 norm and break test (src/osqp_sqp.py:79-91).
 #pragma once
 
+#include <cstddef>
+
 #include "i7m_dynamics.h"
 #include "i7m_indy7_model.h"
 #include "i7m_sincos.h"
@@ -237,6 +239,38 @@ struct LsSplit {
   int* pending = nullptr;     // (B) 1: the second launch finishes this problem
 };
 
+// k_linesearch's kernel arguments as laid out in its kernarg segment (the parameters in order,
+// each at its natural alignment: the C layout of this struct).  With KA, linesearch_body reads the
+// parameters it needs in a round, and everything it needs after the rounds, from there through a
+// laundered scalar pointer (re-loaded by s_load where used) instead of holding them in SGPRs across
+// the candidate rounds, where the baked model's constants already fill the SGPR file and the rest
+// spilled into VGPR lanes (v_writelane / v_readlane, VALU instructions, in every round).
+struct LsKernArgs {
+  const DevModel* Mg;
+  SolveParams P;
+  const double* xu;
+  double* xu_out;
+  const double* sol;
+  const double* goals;
+  const double* fext;
+  int* active;
+  ProblemStats* stats;
+  double* alpha_out;
+  int iter, mode;
+  const double* lin;
+  const double* cost;
+  LsSplit sp;
+};
+static_assert(offsetof(LsKernArgs, P) == 8 && offsetof(LsKernArgs, xu) == 88 && offsetof(LsKernArgs, iter) == 152 &&
+                  offsetof(LsKernArgs, lin) == 160 && offsetof(LsKernArgs, sp) == 176 && sizeof(LsKernArgs) == 200,
+              "LsKernArgs must mirror k_linesearch's kernarg layout (code object metadata: P 8, xu 88, iter 152, "
+              "lin 160, sp 176)");
+__device__ __forceinline__ const LsKernArgs* kernarg_ls() {
+  auto p = __builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (const LsKernArgs*)p;
+}
+
 // W waves per problem (small batches, where the GPU is otherwise idle): wave w evaluates the
 // candidate slots c0 + w R .. c0 + w R + R - 1 of each round, so W R candidates per round (all
 // eight alphas in one round at N = 32, W = 4).  Same first-accept rule, same merits.
@@ -244,7 +278,7 @@ struct LsSplit {
 // The line search of problem b by the W waves of a workgroup (wave w, lane l): the body of
 // k_linesearch, and the third phase of each SQP iteration of k_sqp_fused.  ls_dyn: the dynamic
 // LDS of ls_lds_bytes(T, W); merit: 9 doubles of LDS.
-template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
+template <bool SPEC, int ABL = 0, int W = 1, bool FW = false, bool KA = false>
 __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg, const SolveParams& P, const int b,
                                                 const int w, const int l, double* __restrict__ ls_dyn,
                                                 double* __restrict__ merit, const double* xu, double* xu_out,
@@ -302,6 +336,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   const bool zero_step = __syncthreads_or(step_nz) == 0;
   // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
   // (c0 already offset by this wave's share of the round; `store` false: compute only)
+  double mu_r = P.mu;  // (KA: re-read per round)
   auto reduce_store = [&](double o[4], int c0, bool store) {
     if (pow2) {
       // tree-sum the N knots of each candidate slot with shuffles (segments of width N); the
@@ -313,7 +348,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += t[j];
       }
-      if (store && k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + P.mu * o[3];
+      if (store && k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + mu_r * o[3];
     } else {
       part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
       lds_sync();
@@ -325,7 +360,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
           uc += part[l * N + kk][2];
           cv += part[l * N + kk][3];
         }
-        merit[c0 + l] = qc + vc + uc + P.mu * cv;
+        merit[c0 + l] = qc + vc + uc + mu_r * cv;
       }
     }
     lds_sync();
@@ -374,6 +409,10 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     if (I7M_PRIO & 2) set_prio((c0 - cstart) / (R * W));  // later rounds first: the longest searches
     const int cw = c0 + w * R;  // this wave's first candidate of the round
     const int cand = cw + slot;
+    const LsKernArgs* KR = KA ? kernarg_ls() : nullptr;
+    const SolveParams& PR = KA ? KR->P : P;
+    if (KA) mu_r = PR.mu;
+    const double* f6r = KA ? (KR->fext ? KR->fext + 6L * b : nullptr) : f6;
     double o[4] = {0.0, 0.0, 0.0, 0.0};
     if (slot < R && k < N && cand < 1 + NALPHA) {
       // merit terms of (candidate, knot k): the knot values are recomputed from the LDS copy of
@@ -392,7 +431,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
         o[3] = val(on + 6) + val(ok + 11);
       } else {
-        ls_merit_terms<SPEC, FW>(Mg, P, k, last, base_pt, al, sXD, goal, f6, fpark + l, o);
+        ls_merit_terms<SPEC, FW>(Mg, PR, k, last, base_pt, al, sXD, goal, f6r, fpark + l, o);
       }
       if (k == 0 && cand > 0) {
         // + |XU_new[:12] - XU[:12]|   (src/osqp_sqp.py:63)
@@ -417,40 +456,48 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     }
     lds_sync();
   }
-  if (sp.pending) {
+  // (KA: everything below from the kernarg segment, not held across the rounds)
+  const LsKernArgs* KE = KA ? kernarg_ls() : nullptr;
+  const SolveParams& PE = KA ? KE->P : P;
+  const LsSplit spE = KA ? KE->sp : sp;
+  if (spE.pending) {
     // first launch of a split search: hand an unresolved problem to the second launch
     const int pend = (found < 0 && c_end < 1 + NALPHA) ? 1 : 0;
     if (l == 0 && w == 0) {
-      sp.pending[b] = pend;
-      if (pend) sp.base[b] = merit[0];
+      spE.pending[b] = pend;
+      if (pend) spE.base[b] = merit[0];
     }
     if (pend) return;
   }
   if (W > 1 && w != 0) return;  // one wave applies the step
   const double alpha = (found > 0) ? alphas[found - 1] : 0.0;
-  if (mode == 1) {
-    if (l == 0) alpha_out[b] = alpha;
+  const int modeE = KA ? KE->mode : mode, iterE = KA ? KE->iter : iter;
+  if (modeE == 1) {
+    if (l == 0) (KA ? KE->alpha_out : alpha_out)[b] = alpha;
     return;
   }
-  ProblemStats* st = stats + b;
+  ProblemStats* st = (KA ? KE->stats : stats) + b;
+  int* const actE = KA ? KE->active : active;
+  const double* XE = KA ? KE->xu + (long)b * PE.T : X;
+  double* XOE = KA ? KE->xu_out + (long)b * PE.T : XO;
   if (alpha == 0.0) {
     // src/osqp_sqp.py:81-82: `continue` re-solves the SAME QP from the same XU; the exact
     // solve is deterministic, so every remaining iteration repeats alpha = 0.
     if (l == 0) {
-      for (int it = iter; it < P.max_iters; ++it) st->alphas[st->n_alphas++] = 0.0;
-      st->qp_iters = P.max_iters;
-      active[b] = 0;
+      for (int it = iterE; it < PE.max_iters; ++it) st->alphas[st->n_alphas++] = 0.0;
+      st->qp_iters = PE.max_iters;
+      actE[b] = 0;
     }
-    if (XO != X)
-      for (int e = l; e < P.T; e += 64) XO[e] = sXD[e].x;
+    if (XOE != XE)
+      for (int e = l; e < PE.T; e += 64) XOE[e] = sXD[e].x;
     return;
   }
   double ss = 0.0;
-  for (int e = l; e < P.T; e += 64) {
+  for (int e = l; e < PE.T; e += 64) {
     const XD p = sXD[e];
     const double xv = p.x;
     const double stp = alpha * p.d;
-    XO[e] = xv + stp;
+    XOE[e] = xv + stp;
     ss += stp * stp;
   }
   // wave reduction
@@ -460,13 +507,16 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     const double stepsize = sqrt(ss);
     st->alphas[st->n_alphas++] = alpha;
     st->stepsizes[st->n_steps++] = stepsize;
-    st->qp_iters = iter + 1;
-    if (stepsize < P.step_tol || iter + 1 >= P.max_iters) active[b] = 0;
+    st->qp_iters = iterE + 1;
+    if (stepsize < PE.step_tol || iterE + 1 >= PE.max_iters) actE[b] = 0;
   }
 }
 
 #ifndef I7M_LS_WPE
 #define I7M_LS_WPE 2  // waves per SIMD the line search is compiled for (A/B builds: 3)
+#endif
+#ifndef I7M_LS_KARG
+#define I7M_LS_KARG 1  // k_linesearch re-reads its parameters from the kernarg segment (LsKernArgs)
 #endif
 template <bool SPEC, int ABL = 0, int W = 1, bool FW = false>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(I7M_LS_WPE, I7M_LS_WPE))) k_linesearch(const DevModel* __restrict__ Mg, SolveParams P,
@@ -484,8 +534,9 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(I7M
   if (sp.c_begin > 0 && !sp.pending[b]) return;
   extern __shared__ __attribute__((aligned(16))) double ls_dyn[];
   __shared__ double merit[9];
-  linesearch_body<SPEC, ABL, W, FW>(Mg, P, b, W > 1 ? (int)(threadIdx.x >> 6) : 0, threadIdx.x & 63, ls_dyn, merit, xu,
-                                    xu_out, sol, goals, fext, active, stats, alpha_out, iter, mode, lin, cost, sp);
+  linesearch_body<SPEC, ABL, W, FW, I7M_LS_KARG != 0>(Mg, P, b, W > 1 ? (int)(threadIdx.x >> 6) : 0, threadIdx.x & 63,
+                                                      ls_dyn, merit, xu, xu_out, sol, goals, fext, active, stats,
+                                                      alpha_out, iter, mode, lin, cost, sp);
 }
 
 // Merit pieces of a given XU (hooks for SQP_OSQP.eepos_cost / integrator_err).
