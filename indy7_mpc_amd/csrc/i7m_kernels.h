@@ -138,6 +138,15 @@ struct alignas(16) XD {
 // ahead of its arithmetic.  (As a separate inlined function the kernel allocates spill-free;
 // written in the round loop it spilled, 115 -> 110 us.)
 // FW: f6 is a world-frame wrench, converted to joint 6's frame at this knot's configuration.
+// I7M_LS_NOSEL (default 1): the base point (candidate 0, al = 0) is XU + 0 (sol - XU), equal to XU
+// for every finite step entry but for the sign of an exact zero, so the point values need no
+// per-value select between x and x + al d (two v_cndmask per value, ~100 per evaluation); the
+// base merit of the SQP loop comes from the linearisation anyway, candidate 0 is evaluated only
+// without it.
+#ifndef I7M_LS_NOSEL
+#define I7M_LS_NOSEL 1
+#endif
+__device__ __forceinline__ double ls_pick(bool base_pt, double x, double v) { return (I7M_LS_NOSEL || !base_pt) ? v : x; }
 template <bool SPEC, bool FW = false>
 __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, const SolveParams& P, const int k,
                                                       const bool last, const bool base_pt, const double al,
@@ -150,7 +159,7 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
   auto val = [&](int e) -> double {
     const XD p = sXD[e];
     const double v = p.x + al * p.d;
-    return base_pt ? p.x : v;
+    return ls_pick(base_pt, p.x, v);
   };
   double c[6], sn[6], pe[3];
   {
@@ -176,8 +185,8 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double vi = pv[i].x + al * pv[i].d, ui = pu[i].x + al * pu[i].d;
-      v[i] = base_pt ? pv[i].x : vi;
-      u[i] = base_pt ? pu[i].x : ui;
+      v[i] = ls_pick(base_pt, pv[i].x, vi);
+      u[i] = ls_pick(base_pt, pu[i].x, ui);
       vv += v[i] * v[i];
     }
   }
@@ -214,7 +223,7 @@ __device__ __forceinline__ void ls_merit_terms(const DevModel* __restrict__ Mg, 
       for (int i = 0; i < 3; ++i) {
         auto pt = [&](const XD& p) {
           const double v = p.x + al * p.d;
-          return base_pt ? p.x : v;
+          return ls_pick(base_pt, p.x, v);
         };
         const double xq = pt(pq[i]), xv = pt(pv[i]), nq = pt(pn[i]), nv = pt(pw[i]);
         const double dq = (xq + xv * P.dt) - nq;
@@ -425,7 +434,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
       auto val = [&](int e) -> double {
         const XD p = sXD[e];
         const double v = p.x + al * p.d;
-        return base_pt ? p.x : v;
+        return ls_pick(base_pt, p.x, v);
       };
       if (ABL == 1) {  // diagnostic timing build: dynamics replaced by trivial math
         o[0] = val(ok) * val(ok + 1); o[1] = val(ok + 6) * val(ok + 6); o[2] = val(ok + 12) * val(on);
@@ -443,7 +452,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
           const double vi = p0[i].x + al * p0[i].d;
-          const double t = (base_pt ? p0[i].x : vi) - p0[i].x;
+          const double t = ls_pick(base_pt, p0[i].x, vi) - p0[i].x;
           dd += t * t;
         }
         o[3] += sqrt(dd);
