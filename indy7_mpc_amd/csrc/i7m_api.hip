@@ -77,7 +77,10 @@ struct Timing {
 
 // k_riccati_mfma's Gauss-Jordan pivot broadcasts switch from v_readlane to DPP from this batch
 // size on (riccati_mfma_body BC)
-constexpr int RIC_DPP_MIN_B = 2048;
+// DPP pivot broadcasts at every batch size since the round-3 stage changes (re-measured: 57.9 -> 54.7 us
+// at B = 1024, 44.3 -> 42.6 at 512, 41.4 -> 40.0 at 64, 40.7 -> 39.5 at B = 1; before them they
+// cost ~4.5 us below 2048; profiles/r03_ric_bc_retune_ab.txt)
+constexpr int RIC_DPP_MIN_B = 0;
 constexpr int RIC_W2_MAX_B = 128;     // two-wave Riccati up to this batch size (I7M_RIC_W2 forces): 43.9 -> 42.0 us at B = 1, 44.6 -> 42.7 at 64; slower from 512
 constexpr int RIC_PRIO_MIN_B = 1024;  // as many problems as SIMDs: Riccati waves start sharing SIMDs
 
@@ -312,9 +315,8 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
 #endif
     // (the diag library's default path is the release selection below, so its per-wave timelines
     // show the shipping kernels)
-    // cross-lane broadcasts (riccati_mfma_body BC): the rollout's by DPP at every batch size; the
-    // pivots' by DPP from RIC_DPP_MIN_B problems on (fewer instructions) and by v_readlane below
-    // (shorter chain); I7M_RIC_BC=0..3 forces one (A/B)
+    // cross-lane broadcasts (riccati_mfma_body BC): the rollout's and the pivots' by DPP (from
+    // RIC_DPP_MIN_B problems on, now every size); I7M_RIC_BC=0..3 forces one (A/B)
     // wave priority by progress (BC bit 2) once SIMDs hold more than one wave: -6 % at B = 4096,
     // -4 % at B = 1024 (uneven dispatch puts two waves on some SIMDs), +1 us at B = 64
     const int bc = h->ric_bc >= 0 ? h->ric_bc

@@ -14,6 +14,12 @@
 #ifndef I7M_IPM_WPE
 #define I7M_IPM_WPE 4
 #endif
+// cross-lane broadcasts of the box body's Newton steps (riccati_mfma_body BC): 3 = the rollout's and
+// the pivots' by DPP (5.45 -> 5.42 ms per k_ipm_fused launch against 2, the rollout's only; bit-identical;
+// DESIGN.md §4.2)
+#ifndef I7M_IPM_BC
+#define I7M_IPM_BC 3
+#endif
 
 namespace i7m {
 
@@ -459,8 +465,8 @@ k_ipm_fused(IpmFusedArgs args) {
     __syncthreads();
     if (!DELTA) {
       // the corrector (half 1) stores only K~'s feedforward column: its gain is the predictor's
-      riccati_mfma_body<0, true, false, 2>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
-                                           nullptr, half == 1);
+      riccati_mfma_body<0, true, false, I7M_IPM_BC>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig,
+                                                    A->h, sh, l, nullptr, half == 1);
     } else if (half == 0) {
       riccati_mfma_body<0, true, true>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig, A->h, sh, l,
                                        A->hinv);
