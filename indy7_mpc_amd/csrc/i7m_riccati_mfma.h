@@ -299,11 +299,9 @@ __device__ __forceinline__ double rcp_nr(double d) {
 // BC: cross-lane broadcasts by DPP row_newbcast instead of v_readlane — bit 0 the Gauss-Jordan
 // pivot columns, bit 1 the rollout's x and u; bit-identical either way.  Bit 2: wave priority by
 // progress (ric_prio_back / _fwd), for launches with several waves per SIMD.  Measured (DESIGN.md
-// §4.2): bit 1 helps at every batch size; bit 0 helps at B = 4096 (fewer instructions) and
-// costs ~4.5 us per launch at B <= 256 (a longer pivot chain), so launch_riccati sets it by
-// batch size.  The config-4 body (BOX, k_ipm_fused) takes bit 1 only: with DPP pivots its
-// fused interior-point kernel spills more (10.7 -> 12.2 ms per QP); the DPP rollout alone
-// gives 10.68 -> 10.60 ms.
+// §4.2): bit 1 helps at every batch size; bit 0 cost ~4.5 us per launch at B <= 256 (a longer
+// pivot chain) until the round-3 stage changes, and helps at every batch size since, in the
+// config-4 body (BOX, k_ipm_fused, I7M_IPM_BC) too.
 #ifndef I7M_RIC_PRIO_S
 #define I7M_RIC_PRIO_S 1  // 0: quarters of the backward sweep (A/B: 113.8 vs 112.8 us at B = 4096)
 #endif
