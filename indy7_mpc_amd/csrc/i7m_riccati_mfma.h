@@ -7,7 +7,8 @@
 //     A~ = [[A, c], [0, 1]],  B~ = [B; 0],  Q~ = [[Q, q], [q', 0]],  N~ = [0 | r]
 //     W0 = V~ A~,  Qxx = A~' W0 + Q~,  W1 = V~ B~,  H = B~' W1 + R,  G~ = B~' W0 + N~
 //     K~ = -H^-1 G~  (6x13: [K | kff]),   V~ <- Qxx + K~' G~
-// Sixteen 16x16x4 MFMAs per stage.  V~ never leaves the accumulator registers: it is
+// (First form: sixteen 16x16x4 MFMAs per stage; now 7 of them and 8 4x4x4_4b, I7M_RIC_44 and
+// I7M_QXX_K0_VALU below.)  V~ never leaves the accumulator registers: it is
 // symmetric, so the C/D layout of V~ (lane holds V[(l>>4)+4i][l&15]) is exactly the A-operand
 // layout (V[l&15][4s+(l>>4)]) the next stage needs.  Likewise W0 / W1 / G~ are consumed as
 // B operands straight from their accumulators.  LDS only carries the stage data, H and G~
