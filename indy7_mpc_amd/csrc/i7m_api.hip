@@ -82,7 +82,9 @@ struct Timing {
 // cost ~4.5 us below 2048; profiles/r03_ric_bc_retune_ab.txt)
 constexpr int RIC_DPP_MIN_B = 0;
 constexpr int RIC_W2_MAX_B = 128;     // two-wave Riccati up to this batch size (I7M_RIC_W2 forces): 43.9 -> 42.0 us at B = 1, 44.6 -> 42.7 at 64; slower from 512
-constexpr int RIC_PRIO_MIN_B = 1024;  // as many problems as SIMDs: Riccati waves start sharing SIMDs
+// wave priority by progress once Riccati waves share SIMDs: from 768 problems (re-measured in round 3:
+// 55.2 -> 52.4 us at B = 768, 42.5 -> 43.3 at 512; profiles/r03_ric_bc_retune_ab.txt)
+constexpr int RIC_PRIO_MIN_B = 768;
 
 struct i7m_handle {
   i7m_config cfg;

@@ -219,8 +219,8 @@ def test_riccati_broadcast_variants_bit_identical(lib, model, N, B, monkeypatch)
     row_newbcast with H's columns duplicated in a second 16-lane row for the pivots) move the
     same values: whole solves are bit-identical for every variant (I7M_RIC_BC=0..3), and with the
     progress-priority bit (6, 7: s_setprio per stage changes only the issue order); B = 2050
-    also runs the automatic choice (DPP pivots from 2048 problems, DPP rollout always, priority
-    above 1024)."""
+    also runs the automatic choice (DPP pivots and rollout at every size, priority from 768
+    problems)."""
     xcur, goals, XU = synthetic_batch(B, N, seed=600 + N + B)
     outs = {}
     for bc in ("0", "1", "2", "3", "6", "7", "auto"):
