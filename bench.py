@@ -191,6 +191,7 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
     kt = h.kernel_times()
     it, conv, _ = h.box_stats(B)
     out = t_out.cpu().numpy()
+    h.close()
     return {"workload": f"config4: B={B}, N={N}, box rows on q/v/u (URDF limits), interior-point QP",
             "value": B * steps / el, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
             "ipm_iters_last_qp_mean": float(it.mean()), "ipm_converged_frac": float(conv.mean()),
