@@ -122,7 +122,7 @@ struct i7m_handle {
   unsigned long long graph_clock = 0;
   bool use_graph = false;  // I7M_GRAPH=1: capture the solve once per buffer set, replay it
                            // (measured 4-5 us slower per solve at B = 1 and 64, level at 4096)
-  int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 256), else I7M_LS_WAVES (1, 2 or 4)
+  int ls_waves = 0;  // waves per problem in k_linesearch: 0 automatic (4 for B <= 768), else I7M_LS_WAVES (1, 2 or 4)
   // I7M_LS_TAIL = r > 0: split line search — the first launch (one wave per problem) stops after r
   // rounds, a second launch with two waves per problem finishes the unresolved problems
   int ls_tail = 0;
@@ -350,7 +350,13 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
 }
 
 // waves per problem of the line search (k_linesearch) and of k_sqp_fused
-int waves_for(const i7m_handle* h, int B) { return h->ls_waves > 0 ? h->ls_waves : (B <= 256 ? 4 : 1); }
+// (k_linesearch: 4 waves per problem up to 768 problems — re-measured in round 3: 28.2 -> 19.0 us at
+// B = 384, 28.6 -> 19.8 at 512, 29.9 -> 28.8 at 768, 30.6 -> 35.2 at 1024, profiles/r03_ls_waves_ab.txt;
+// k_sqp_fused keeps the 256 it was measured with)
+constexpr int LS_W4_MAX_B = 768, FUSED_W4_MAX_B = 256;
+int waves_for(const i7m_handle* h, int B, int max_b4 = LS_W4_MAX_B) {
+  return h->ls_waves > 0 ? h->ls_waves : (B <= max_b4 ? 4 : 1);
+}
 
 // base_from_lin: lin/cost of W hold the linearisation of this xu (the SQP loop), so the base
 // merit comes from them (k_linesearch); otherwise candidate 0 is evaluated.
@@ -491,7 +497,7 @@ bool use_fused(const i7m_handle* h, int B) {
 
 int launch_fused(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu_in, double* xu_out,
                  const double* xs, const double* goals, ProblemStats* st, long b0) {
-  const int nw = waves_for(h, P.B);
+  const int nw = waves_for(h, P.B, FUSED_W4_MAX_B);
   // I7M_PIPE_FUSED_ITER: one launch per SQP iteration, else one per solve
   const int launches = h->pipeline == I7M_PIPE_FUSED_ITER ? h->cfg.max_sqp_iters : 1;
   for (int i = 0; i < launches; ++i) {

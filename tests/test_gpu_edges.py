@@ -328,9 +328,9 @@ def test_chunked_host_to_host_solve_bit_identical(lib, model, monkeypatch, chunk
 def test_split_line_search_bit_identical(lib, model, monkeypatch, tail):
     """I7M_LS_TAIL=r: the line search as two launches — r rounds of one wave per problem, then
     two waves per problem for the problems that have not accepted a candidate (base merit handed
-    over) — gives the one-launch search's alphas, stats and XU bit for bit (B = 300 > 256, so the
+    over) — gives the one-launch search's alphas, stats and XU bit for bit (B = 800 > 768, so the
     one-wave kernel is the reference; both wrench frames)."""
-    B, N = 300, 32
+    B, N = 800, 32
     xcur, goals, XU = synthetic_batch(B, N, seed=90 + int(tail))
     fx = np.random.default_rng(3).normal(0.0, 20.0, (B, 6))
     outs = {}
