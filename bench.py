@@ -159,10 +159,15 @@ def _pmc_traffic(kernel: str, B: int, N: int):
         return None
 
 
-def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N: int = 64):
+def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N: int = 64, native=None,
+            cpu_budget: float = 10.0, cpu_threads: int = 1):
     """SURVEY.md §8d config 4 (extension, no reference number): B problems, N knots, box rows on
     q, v, u (URDF limits), interior-point QP mode (I7M_QP_BOX).  Device-resident inputs, same
-    step definition as the headline; reported as an extra object, not as `value`."""
+    step definition as the headline; reported as an extra object, not as `value`.  With `native`
+    (rank 0 at N = 1) it also carries the C++ port's box mode as `cpu_baseline` (a bounded sample,
+    1 thread and the job's share), `parity_vs_port` (all B problems of the last timed step against
+    the port on the same inputs) and the `roofline` of `k_ipm_fused` (HBM of record: 312 N B per
+    problem per launch; FP64 beside it from the port's instrumented interior-point flops)."""
     import torch
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.synthetic import make_batch
@@ -173,9 +178,10 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
     xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 4)
     t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
     t_out = torch.empty_like(t_xu)
+    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
 
     def step():
-        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
 
     for _ in range(warmup):
         step()
@@ -191,12 +197,70 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
     kt = h.kernel_times()
     it, conv, _ = h.box_stats(B)
     out = t_out.cpu().numpy()
+    st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
     h.close()
-    return {"workload": f"config4: B={B}, N={N}, box rows on q/v/u (URDF limits), interior-point QP",
-            "value": B * steps / el, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
-            "ipm_iters_last_qp_mean": float(it.mean()), "ipm_converged_frac": float(conv.mean()),
-            "finite": bool(np.isfinite(out).all()),
-            "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
+    res = {"workload": f"config4: B={B}, N={N}, box rows on q/v/u (URDF limits), interior-point QP",
+           "value": B * steps / el, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
+           "ipm_iters_last_qp_mean": float(it.mean()), "ipm_converged_frac": float(conv.mean()),
+           "qp_iters_mean": float(st["qp_iters"].mean()),
+           "finite": bool(np.isfinite(out).all()),
+           "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
+    # roofline of the dominant kernel (k_ipm_fused: one launch per QP, every active problem)
+    dom = max(kt, key=lambda k: kt[k][0])
+    dom_ms, dom_cnt = kt[dom]
+    dom_avg_s = dom_ms / max(dom_cnt, 1) / 1e3
+    ppl = float(st["qp_iters"].sum()) / max(dom_cnt // steps, 1)
+    ab = algorithmic_bytes(N)
+    achieved = ppl * ab / dom_avg_s / 1e9
+    traffic = _pmc_traffic(dom, B, N)
+    res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                       "traffic_over_algorithmic": None if traffic is None else traffic / (ppl * ab),
+                       "algorithmic_bytes_per_problem": ab, "algorithmic_source": "SURVEY.md 8d: 312 N B per solve",
+                       "problems_per_launch": ppl, "avg_launch_us": dom_avg_s * 1e6,
+                       "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"}
+    if native is not None:
+        from oracle import cpu
+        lib_path, build_desc = native
+        cpu.load(lib_path)
+        # parity: the port's box mode on exactly these inputs, every problem
+        ref, qp, al, _, rit, rconv, _ = cpu.solve_box(xcur, goals, XU, N, nthreads=cpu_threads)
+        rel = np.linalg.norm(out - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
+        ga = st["alphas"][:, :al.shape[1]]
+        used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
+        used_c = ~np.isnan(al)
+        same_alpha = np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == al, True), axis=1)
+        res["parity_vs_port"] = {
+            "problems": int(B), "alpha_sequence_agreement": float(same_alpha.mean()),
+            "qp_iters_agreement": float((st["qp_iters"] == qp).mean()),
+            "ipm_iters_agreement": float((it == rit[np.arange(B), qp - 1]).mean()),
+            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
+            "reference": "oracle/cpp/i7m_cpu.cpp box mode (oracle/box_ipm.py restated, Riccati Newton steps)"}
+        # CPU baseline: a bounded sample of the same draws, 1 thread and the job's share
+        t0 = time.perf_counter()
+        cpu.solve_box(xcur[:4], goals[:4], XU[:4], N, nthreads=1)
+        per = (time.perf_counter() - t0) / 4
+        n = int(max(4, min(B, cpu_budget / 2 / per)))
+        t0 = time.perf_counter()
+        cpu.solve_box(xcur[:n], goals[:n], XU[:n], N, nthreads=1)
+        t1 = time.perf_counter()
+        nm = min(B, n * cpu_threads)
+        t2 = time.perf_counter()
+        cpu.solve_box(xcur[:nm], goals[:nm], XU[:nm], N, nthreads=cpu_threads)
+        t3 = time.perf_counter()
+        res["cpu_baseline"] = {
+            "value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{n} config-4 solves (the first {n} of these draws, N={N}, box rows) by oracle/cpp/i7m_cpu.cpp "
+                      f"box mode, 1 thread, {t1 - t0:.1f}s",
+            "build": build_desc,
+            "all_cores": {"value": nm / (t3 - t2), "cores": cpu_threads, "sample": f"{nm} solves, {cpu_threads} threads"}}
+        fl = [cpu.count_flops(xcur[b], goals[b], XU[b], N, box=cpu.box_cfg()) for b in range(8)]
+        ipm_per_qp = float(np.mean([f["ipm"] / f["iters"] for f in fl]))
+        a_tf = ppl * ipm_per_qp / dom_avg_s / 1e12
+        res["roofline_fp64"] = {"bound": "fp64", "kernel": dom, "achieved": a_tf, "peak": FP64_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": a_tf / FP64_PEAK_TFLOPS, "flops_per_problem": ipm_per_qp,
+                                "flops_source": "port's instrumented interior-point flops per QP (8 problems)"}
+    return res
 
 
 def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: int = 32):
@@ -258,6 +322,31 @@ def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps
     return {"workload": f"closed-loop MPC: B={B} instances, N={N}, {steps} MPC steps (SQP + rk4 plant + shift)",
             "value": B * steps / el, "unit": "instance-steps/s", "ms_per_mpc_step": 1e3 * el / steps,
             "instances_alive_at_end": int(np.isfinite(d[-1]).sum()), "finite": bool(np.isfinite(q[np.isfinite(q)]).all())}
+
+
+def gather_rank_rows(dist, device: int, elapsed_s: float, h2h_solves_per_s: float):
+    """[device, own pass-1 elapsed, own host-to-host rate] of every rank, in rank order (gloo
+    all_gather; `dist` None = one rank)."""
+    import torch
+
+    row = [float(device), float(elapsed_s), float(h2h_solves_per_s)]
+    if dist is None:
+        return [row]
+    parts = [torch.zeros(3, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, torch.tensor(row, dtype=torch.float64))
+    return [p.tolist() for p in parts]
+
+
+def per_rank_summary(rows, B: int, steps: int):
+    """The line's `per_rank` object (world > 1): rank imbalance (min / median / max of the ranks'
+    own barrier-to-barrier times) and each rank's solve and host-to-host rates, so PCIe
+    contention and slow ranks show on the first real multi-GPU run."""
+    els = [r[1] for r in rows]
+    return {"elapsed_s": {"min": min(els), "median": statistics.median(els), "max": max(els)},
+            "ranks": [{"rank": i, "device": int(r[0]), "elapsed_s": r[1], "solves_per_s": B * steps / r[1],
+                       "host_to_host_solves_per_s": r[2]} for i, r in enumerate(rows)],
+            "note": "elapsed_s: each rank's own barrier-to-barrier time of pass 1 (value uses the max over ranks); "
+                    "host_to_host_solves_per_s: each rank's median host-to-host call, all ranks copying at once"}
 
 
 def launch_ranks(args, argv) -> int:
@@ -403,17 +492,18 @@ def main():
         el = time.perf_counter() - t0
         if kernel_events:
             h.set_timing(False)
+        own = el
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        return el
+        return el, own
 
     # pass 1: `value` — nothing but the solves between the barriers
-    elapsed = timed_pass(False)
+    elapsed, own_el = timed_pass(False)
     # pass 2: the same K steps with per-step events (p50) and per-launch start/stop events on
     # each kernel's dispatch (hipExtLaunchKernelGGL): per-kernel durations for the roofline
-    elapsed_ev = timed_pass(True)
+    elapsed_ev, _ = timed_pass(True)
     step_ms = [a.elapsed_time(b) for a, b in evs]
     ktimes = h.kernel_times()
 
@@ -440,12 +530,11 @@ def main():
         if i >= 3:
             h2h.append(time.perf_counter() - a)
 
-    # the devices the ranks actually ran on (a --share-devices rehearsal puts several on one)
-    devs = [local]
-    if world > 1:
-        parts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-        dist.all_gather(parts, torch.tensor([local], dtype=torch.int64))
-        devs = [int(p.item()) for p in parts]
+    # the devices the ranks actually ran on (a --share-devices rehearsal puts several on one), and
+    # each rank's own elapsed time and host-to-host rate (rank imbalance and PCIe contention show
+    # on the first real multi-GPU run)
+    rank_rows = gather_rank_rows(dist if world > 1 else None, local, own_el, B / statistics.median(h2h))
+    devs = [int(r[0]) for r in rank_rows]
 
     if rank != 0:
         if world > 1:
@@ -468,7 +557,8 @@ def main():
     per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c,
                       "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)} for k, (ms, c) in ktimes.items()}
     cpu = None if native is None else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads, native)
-    c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1)
+    c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1,
+                                                            native=native, cpu_threads=args.cpu_threads)
     c2 = None if (args.no_config2 or world > 1) else config2(model, stream, local, 200, 10)
     mpc = None if (args.no_config2 or world > 1) else mpc_closed_loop(model, stream, local, B, N)
     out = {
@@ -490,10 +580,18 @@ def main():
                                + ", full SQP (<=2 QP + line search), exact KKT",
                    "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)",
                    "devices_used": sorted(set(devs)), "shared_devices": len(set(devs)) < world,
-                   "value_definition": "device-resident: inputs already in HBM, B*world*steps / (max over ranks of "
-                                       "the barrier-to-barrier wall time of K back-to-back solves); BASELINE.md 4's "
-                                       "host-to-host rate (H2D + solve + D2H, median) is host_to_host_solves_per_s"},
+                   "value_definition": "device-resident: inputs already in HBM when the timed region starts, "
+                                       "B*world*steps / (max over ranks of the barrier-to-barrier wall time of K "
+                                       "back-to-back solves) -- the task contract's definition of `value` (measurement "
+                                       "section: 'value is whole-job throughput with inputs already resident in HBM "
+                                       "when the timed region starts ... the PCIe-inclusive rate ... is never value'); "
+                                       "BASELINE.md 4's host-to-host rate (H2D + solve + D2H, median of 20 calls after "
+                                       "3 warm-up) is host_to_host_solves_per_s, its p50 p50_latency_h2h_ms"},
         "p50_latency_ms": statistics.median(step_ms),
+        "p50_latency_definition": "p50_latency_ms: device time per batched step (HIP events on the solve stream); "
+                                  "p50_latency_h2h_ms: BASELINE.md 4's p50 of the host-to-host batched call; "
+                                  "p50_latency_b1_ms: host-to-host B = 1 call (device-resident input)",
+        "p50_latency_h2h_ms": 1e3 * statistics.median(h2h),
         "kernel_timing": {"pass": "second pass of the same K steps with per-launch HIP events on each kernel's dispatch",
                           "value_during_event_pass": B * world * args.steps / elapsed_ev},
         "p50_latency_b1_ms": statistics.median(lat),
@@ -512,6 +610,8 @@ def main():
                            "unit": "GB/s", "frac": value * ab / 1e9 / (HBM_PEAK_GBS * world),
                            "bytes_per_solve": ab},
     }
+    if world > 1:
+        out["per_rank"] = per_rank_summary(rank_rows, B, args.steps)
     if cpu is not None:
         # parity at bench scale: the C++ port on exactly the GPU's inputs (all B problems of
         # this rank), against the last timed step's output and stats

@@ -68,11 +68,14 @@ extern "C" {
 #define I7M_MAX_SQP 8
 #define I7M_MAX_N 64
 
-/* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature or struct
- * layout changes.  2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and
- * i7m_set_external_wrench a trailing `frame` (0.2 builds); 1 had neither.  A caller built against
- * another revision must not call through this library: compare first. */
-#define I7M_ABI_VERSION 2
+/* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
+ * layout, field meaning or enum count changes.  3: i7m_config's former `pad` is `h2h_chunks` (a
+ * nonzero value changes how i7m_solve runs; outside [0, 64] it is refused) and I7M_K_COUNT is 8
+ * (I7M_K_LINESEARCH_TAIL added) — size timing arrays from I7M_K_COUNT of this header (0.3 builds).
+ * 2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and i7m_set_external_wrench a
+ * trailing `frame` (0.2 builds); 1 had neither.  A caller built against another revision must not
+ * call through this library: compare first. */
+#define I7M_ABI_VERSION 3
 
 #define I7M_OK 0
 #define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */

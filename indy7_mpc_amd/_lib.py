@@ -20,7 +20,7 @@ import numpy as np
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
-ABI_VERSION = 2  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
+ABI_VERSION = 3  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8
 MAX_N = 64

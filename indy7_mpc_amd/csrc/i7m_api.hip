@@ -48,7 +48,7 @@ hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipSt
                                 const void* model, const void* params, const double* xu_in, double* xu_out,
                                 const double* xs, const double* goals, const double* fext, double* lin, double* cost,
                                 double* qpd, double* kbuf, double* sol, int* active, void* stats);
-hipError_t i7m_prepare_sqp_fused();
+hipError_t i7m_prepare_sqp_fused(int dev, int N);
 
 static_assert(sizeof(i7m_problem_stats) == sizeof(ProblemStats), "stats layout");
 
@@ -617,9 +617,8 @@ int copy_out(i7m_handle* h, double* dst, const double* src, size_t n, hipStream_
 int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
                         int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch);
 
-int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals, int goal_stride,
-                      double* xu_out, i7m_problem_stats* stats, int nch) {
-  if (h->h2h_pipe) return solve_h2h_pipelined(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch);
+int solve_h2h_chunked_body(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
+                           int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch) {
   const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
   int rc;
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
@@ -657,8 +656,8 @@ int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* x
 // i in, and chunk i-1 out, while the device solves the chunk before.  The alternating two-stream
 // layout above issued all copy-ins at once: they shared the link and finished together, then the
 // solves ran, then the copy-outs — no overlap.
-int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
-                        int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch) {
+int solve_h2h_pipelined_body(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
+                             int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch) {
   const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
   while ((int)h->ev_in.size() < nch) {
     hipEvent_t a = nullptr, b = nullptr;
@@ -764,6 +763,30 @@ int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double*
   HIPCHK(hipStreamWaitEvent(h->stream, h->ev_done[1], 0));
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
+}
+
+// Error exit of a chunked call: chunks already queued on cs[0], cs[1] and cs2 keep
+// running after a failed call returns, and their copies out could land in caller memory after the
+// error (or race the next call's copies in, which order only after h->stream).  So every error
+// return waits for all the streams the chunks use (their own errors ignored; the first message kept).
+int drain_after_error(i7m_handle* h, int rc) {
+  if (rc == I7M_OK) return rc;
+  const std::string msg = g_err;
+  for (int c = 0; c < 2; ++c)
+    if (h->cs[c]) (void)hipStreamSynchronize(h->cs[c]);
+  if (h->cs2) (void)hipStreamSynchronize(h->cs2);
+  (void)hipStreamSynchronize(h->stream);
+  g_err = msg;
+  return rc;
+}
+int solve_h2h_pipelined(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals,
+                        int goal_stride, double* xu_out, i7m_problem_stats* stats, int nch) {
+  return drain_after_error(h, solve_h2h_pipelined_body(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch));
+}
+int solve_h2h_chunked(i7m_handle* h, int B, const double* xu_in, const double* xcur, const double* goals, int goal_stride,
+                      double* xu_out, i7m_problem_stats* stats, int nch) {
+  if (h->h2h_pipe) return solve_h2h_pipelined(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch);
+  return drain_after_error(h, solve_h2h_chunked_body(h, B, xu_in, xcur, goals, goal_stride, xu_out, stats, nch));
 }
 
 }  // namespace
@@ -892,7 +915,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
                    : std::strcmp(e, "split") == 0 ? I7M_PIPE_SPLIT
                    : h->pipeline;
   if (h->pipeline == I7M_PIPE_FUSED || h->pipeline == I7M_PIPE_FUSED_ITER) {
-    const hipError_t ef = i7m_prepare_sqp_fused();
+    const hipError_t ef = i7m_prepare_sqp_fused(h->dev, cfg->N);
     if (ef != hipSuccess) return bail(fail(I7M_EHIP, std::string("k_sqp_fused LDS limit: ") + hipGetErrorString(ef)));
   }
   const size_t Bm = (size_t)cfg->max_batch, N = (size_t)cfg->N, T = 18 * N - 6;

@@ -214,7 +214,8 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
   s01 = wave_sum(s01);
   s10 = wave_sum(s10);
   s11 = wave_sum(s11);
-  const double mua = ((s00 + ad * s01) + ap * (s10 + ad * s11)) / (2.0 * S.nb);
+  // clamped at 0: near convergence s00 ~ 2 nb mu cancels against the other sums
+  const double mua = fmax(((s00 + ad * s01) + ap * (s10 + ad * s11)) / (2.0 * S.nb), 0.0);
   const double r = mua / S.mu;
   const double smu = r * r * r * S.mu;
   // pass 2: the corrector's linear-term shift h

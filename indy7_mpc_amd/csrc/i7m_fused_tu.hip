@@ -4,6 +4,7 @@
 #include <hip/hip_ext.h>
 
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <type_traits>
 
@@ -49,35 +50,41 @@ hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipSt
 }
 
 // Raise every k_sqp_fused instantiation's dynamic-LDS limit beyond the 64 KB default (four waves
-// hold four linearisation regions) to what the largest horizon needs, once per process; called
-// by i7m_create for a handle that may run the fused pipeline, so launches (and graph captures)
-// never call hipFuncSetAttribute.
-hipError_t i7m_prepare_sqp_fused() {
+// hold four linearisation regions) to what a horizon of N knots needs, on device `dev`; called by
+// i7m_create for a handle that may run the fused pipeline, so launches (and graph captures) never
+// call hipFuncSetAttribute.  The limit is per device: one record per device id of the largest
+// horizon raised so far, so a second handle on another device (or with a longer horizon) raises
+// its own, and a failure is not cached for later handles.
+hipError_t i7m_prepare_sqp_fused(int dev, int N) {
   using namespace i7m;
-  static std::once_flag once;
-  static hipError_t err = hipSuccess;
-  std::call_once(once, [] {
-    auto set = [](auto kern, int W) {
-      const int lds = (int)fused_lds_bytes(18 * I7M_MAX_N - 6, W);
-      const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e != hipSuccess && err == hipSuccess) err = e;
-    };
-    set(k_sqp_fused<true, 1, false, false>, 1);
-    set(k_sqp_fused<true, 1, false, true>, 1);
-    set(k_sqp_fused<true, 1, true, false>, 1);
-    set(k_sqp_fused<true, 1, true, true>, 1);
-    set(k_sqp_fused<false, 1, false, false>, 1);
-    set(k_sqp_fused<false, 1, false, true>, 1);
-    set(k_sqp_fused<false, 1, true, false>, 1);
-    set(k_sqp_fused<false, 1, true, true>, 1);
-    set(k_sqp_fused<true, 4, false, false>, 4);
-    set(k_sqp_fused<true, 4, false, true>, 4);
-    set(k_sqp_fused<true, 4, true, false>, 4);
-    set(k_sqp_fused<true, 4, true, true>, 4);
-    set(k_sqp_fused<false, 4, false, false>, 4);
-    set(k_sqp_fused<false, 4, false, true>, 4);
-    set(k_sqp_fused<false, 4, true, false>, 4);
-    set(k_sqp_fused<false, 4, true, true>, 4);
-  });
+  static std::mutex mu;
+  static std::map<int, int> raised;  // device id -> horizon the limits cover
+  std::lock_guard<std::mutex> lock(mu);
+  const auto it = raised.find(dev);
+  if (it != raised.end() && it->second >= N) return hipSuccess;
+  hipError_t err = hipSetDevice(dev);
+  if (err != hipSuccess) return err;
+  auto set = [&](auto kern, int W) {
+    const int lds = (int)fused_lds_bytes(18 * N - 6, W);
+    const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess && err == hipSuccess) err = e;
+  };
+  set(k_sqp_fused<true, 1, false, false>, 1);
+  set(k_sqp_fused<true, 1, false, true>, 1);
+  set(k_sqp_fused<true, 1, true, false>, 1);
+  set(k_sqp_fused<true, 1, true, true>, 1);
+  set(k_sqp_fused<false, 1, false, false>, 1);
+  set(k_sqp_fused<false, 1, false, true>, 1);
+  set(k_sqp_fused<false, 1, true, false>, 1);
+  set(k_sqp_fused<false, 1, true, true>, 1);
+  set(k_sqp_fused<true, 4, false, false>, 4);
+  set(k_sqp_fused<true, 4, false, true>, 4);
+  set(k_sqp_fused<true, 4, true, false>, 4);
+  set(k_sqp_fused<true, 4, true, true>, 4);
+  set(k_sqp_fused<false, 4, false, false>, 4);
+  set(k_sqp_fused<false, 4, false, true>, 4);
+  set(k_sqp_fused<false, 4, true, false>, 4);
+  set(k_sqp_fused<false, 4, true, true>, 4);
+  if (err == hipSuccess) raised[dev] = N;
   return err;
 }

@@ -71,6 +71,7 @@ class IPMResult:
     converged: bool
     mu: list = field(default_factory=list)
     alpha: list = field(default_factory=list)
+    mua: list = field(default_factory=list)  # per iteration: (expanded mu_aff, direct product sum, mu)
 
 
 def _ratio(v, dv, bm):
@@ -124,6 +125,12 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
         s10 = float(np.sum((dxa * zl - dxa * zu)[bm]))
         s11 = float(np.sum((dxa * dzla - dxa * dzua)[bm]))
         mua = ((s00 + ad * s01) + ap * (s10 + ad * s11)) / (2 * nb)
+        # the direct product sum, independent of the expansion (tests/test_box_oracle.py pins the
+        # two together); near convergence s00 ~ 2 nb mu cancels against the other terms, so the
+        # expanded form is clamped at 0 (a negative sigma mu would push away from the centre)
+        mua_direct = float(np.sum(((sl + ap * dxa) * (zl + ad * dzla) + (su - ap * dxa) * (zu + ad * dzua))[bm])) / (2 * nb)
+        res.mua.append((mua, mua_direct, mu))
+        mua = max(mua, 0.0)
         smu = (mua / mu) ** 3 * mu
         # corrector
         rl = np.where(bm, sl * zl + dxa * dzla - smu, 0.0)

@@ -15,6 +15,9 @@
 //   riccati                          the equality-constrained QP (:137-143), exact
 //   merit / linesearch               eepos_cost, integrator_err, linesearch (src/osqp_sqp.py:13-74)
 //   sqp                              src/osqp_sqp.py:76-93
+//   ipm (box_mask != 0)              config 4's box rows (no reference
+//                                    counterpart): oracle/box_ipm.py::ipm_box, Newton steps by
+//                                    riccati with the (Sigma, h) shifts, as i7m_box.h on the GPU
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -62,6 +65,7 @@ template <class R> inline Dual<R> operator*(R a, Dual<R> b) { return {a * b.v, a
 
 struct Model {
   double Rp[6][9], tp[6][3], m[6], h[6][3], Io[6][6], g[3];
+  double qlo[6], qhi[6], vlim[6], ulim[6];  // description/indy7.urdf:203-238 <limit>
 };
 
 Model make_model(const double* p) {
@@ -89,6 +93,12 @@ Model make_model(const double* p) {
     M.Io[i][5] = Ic[5] + mass[i] * (cc - c[2] * c[2]);
   }
   for (int k = 0; k < 3; ++k) M.g[k] = g[k];
+  for (int k = 0; k < 6; ++k) {
+    M.qlo[k] = p[135 + k];
+    M.qhi[k] = p[141 + k];
+    M.vlim[k] = p[147 + k];
+    M.ulim[k] = p[153 + k];
+  }
   return M;
 }
 
@@ -310,6 +320,9 @@ void fk_jac(const Model& Md, const R* c, const R* s, R* p, R J[3][6]) {
 struct Params {
   int N, regularize, max_iters, goal_stride;
   double dt, dQ, R, QN, eps, mu, step_tol;
+  // config 4 box rows (oracle/box_ipm.py; 0 = the reference's equality-only QP)
+  int box_mask, box_max_iters;
+  double box_tol, box_theta, box_eta, box_z0;
 };
 
 template <class R>
@@ -318,11 +331,18 @@ struct Solver {
   Params P;
   int T;
   std::vector<R> lin, cost, K, sol;  // lin (N-1)*114, cost N*10, K (N-1)*84
+  // box mode: the interior point's iterate, bound duals, Newton shifts and predictor step
+  std::vector<R> bx, bzl, bzu, bsig, bh, bdxa;
+  int ipm_iters = 0, ipm_conv = 0;
+  double ipm_mu = 0.0;
   Solver(const Model& m, const Params& p) : Md(m), P(p), T(18 * p.N - 6) {
     lin.resize((P.N - 1) * 114);
     cost.resize(P.N * 10);
     K.resize((P.N - 1) * 84);
     sol.resize(T);
+    if (P.box_mask) {
+      bx.resize(T); bzl.resize(T); bzu.resize(T); bsig.resize(T); bh.resize(T); bdxa.resize(T);
+    }
   }
 
   // Analytic world-frame O(n^2) derivatives (the algorithm of the GPU's k_linearize,
@@ -561,7 +581,9 @@ struct Solver {
     }
   }
 
-  void riccati(const R* X, const R* xs) {
+  // sg / hs (box mode): the interior point's Newton step solves the same QP with Hessian
+  // P + diag(sg) and linear term g + hs (oracle/box_ipm.py, i7m_box.h); null = the plain QP.
+  void riccati(const R* X, const R* xs, const R* sg = nullptr, const R* hs = nullptr) {
     const int N = P.N;
     const R dt = R(P.dt);
     R V[12][12], v[12];
@@ -569,6 +591,11 @@ struct Solver {
     for (int r = 0; r < 12; ++r)
       for (int c = 0; c < 12; ++c) V[r][c] = (r < 6 && c < 6) ? cw[6] * (cw[r] * cw[c]) : (r == c ? cw[7] : R(0));
     for (int r = 0; r < 12; ++r) v[r] = r < 6 ? cw[6] * cw[r] : cw[7] * X[18 * (N - 1) + r];
+    if (sg)
+      for (int r = 0; r < 12; ++r) {
+        V[r][r] = V[r][r] + sg[18 * (N - 1) + r];
+        v[r] = v[r] + hs[18 * (N - 1) + r];
+      }
     for (int k = N - 2; k >= 0; --k) {
       const R* L = &lin[114 * k];
       const R* w = &cost[10 * k];
@@ -614,19 +641,22 @@ struct Solver {
           for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * VA[6 + m][c];
           G[r][c] = acc;
         }
+      const R* sgk = sg ? sg + 18 * k : nullptr;
+      const R* hsk = sg ? hs + 18 * k : nullptr;
       for (int r = 0; r < 6; ++r)
         for (int c = r; c < 6; ++c) {
-          R acc = r == c ? w[8] : R(0);
+          R acc = r == c ? (sgk ? w[8] + sgk[12 + r] : w[8]) : R(0);
           for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * Tm[m][c];
           H[r][c] = H[c][r] = acc;
         }
       for (int r = 0; r < 6; ++r) {
-        R acc = w[8] * x[12 + r];
+        R acc = sgk ? w[8] * x[12 + r] + hsk[12 + r] : w[8] * x[12 + r];
         for (int m = 0; m < 6; ++m) acc = acc + Bu[6 * m + r] * s_[6 + m];
         h[r] = acc;
       }
       for (int r = 0; r < 12; ++r) {
         R acc = r < 6 ? w[6] * w[r] + s_[r] : w[7] * x[6 + r - 6] + dt * s_[r - 6];
+        if (sgk) acc = acc + hsk[r];
         for (int m = 0; m < 6; ++m) acc = acc + (r < 6 ? Aq[6 * m + r] : Av[6 * m + r - 6]) * s_[6 + m];
         vA[r] = acc;
       }
@@ -644,6 +674,7 @@ struct Solver {
           R acc = AtVA[r][c];
           if (r < 6 && c < 6) acc = acc + w[6] * (w[r] * w[c]);
           else if (r == c) acc = acc + w[7];
+          if (sgk && r == c) acc = acc + sgk[r];
           for (int m = 0; m < 6; ++m) acc = acc + G[m][r] * Kk[12 * m + c];
           V[r][c] = V[c][r] = acc;
         }
@@ -674,6 +705,143 @@ struct Solver {
       }
       for (int i = 0; i < 12; ++i) sol[18 * (k + 1) + i] = xk[i] = xn[i];
     }
+  }
+
+  // ---- config 4: the box-constrained QP by Mehrotra predictor-corrector (oracle/box_ipm.py
+  // ::ipm_box, step for step as i7m_box.h's ipm_init/pred/corr bodies), every Newton step the
+  // Riccati solve above with the (Sigma, h) shifts; equality rows exact.  sol holds x_eq on
+  // entry and the box-QP minimiser on exit.
+  bool box_of(int e, double& lo, double& hi) const {
+    const int k = e / 18, j = e - 18 * k;
+    if (k == 0 && j < 12) return false;  // the fixed initial state
+    if (j < 6) {
+      if (!(P.box_mask & 1)) return false;
+      lo = Md.qlo[j]; hi = Md.qhi[j];
+    } else if (j < 12) {
+      if (!(P.box_mask & 2)) return false;
+      hi = Md.vlim[j - 6]; lo = -hi;
+    } else {
+      if (!(P.box_mask & 4)) return false;
+      hi = Md.ulim[j - 12]; lo = -hi;
+    }
+    return true;
+  }
+  static R ratio_min(R t, R v, R dv) {
+    if (!(dv < R(0))) return t;
+    const R q = -v / dv;
+    return q < t ? q : t;
+  }
+
+  void ipm(const R* X, const R* xs) {
+    const double theta = P.box_theta, z0 = P.box_z0;
+    // init (ipm_init_body): x = clip(x_eq) into the interior, centred duals z = z0 / s
+    R acc = R(0);
+    int nb = 0;
+    for (int e = 0; e < T; ++e) {
+      double lo, hi;
+      R xv = sol[e], a = R(0), c = R(0), s = R(0);
+      if (box_of(e, lo, hi)) {
+        const double w = hi - lo;
+        const double l1 = lo + theta * w, h1 = hi - theta * w;
+        if (xv < R(l1)) xv = R(l1);
+        if (R(h1) < xv) xv = R(h1);
+        const R sl = xv - R(lo), su = R(hi) - xv;
+        a = R(z0) / sl;
+        c = R(z0) / su;
+        acc = acc + (sl * a + su * c);
+        s = a / sl + c / su;
+        ++nb;
+      }
+      bx[e] = xv; bzl[e] = a; bzu[e] = c; bsig[e] = s;
+      bh[e] = -(s * xv);
+    }
+    R mu = nb ? acc / R(2.0 * nb) : R(0);
+    double rfrac = 1.0;
+    int it = 0;
+    bool conv = nb == 0;
+    while (!conv && it < P.box_max_iters) {
+      // predictor Newton step (tau = 0): y = argmin with l = g - Sigma x
+      riccati(X, xs, bsig.data(), bh.data());
+      R ap = R(1), ad = R(1), s00 = R(0), s01 = R(0), s10 = R(0), s11 = R(0);
+      for (int e = 0; e < T; ++e) {
+        const R d = sol[e] - bx[e];
+        bdxa[e] = d;
+        double lo, hi;
+        if (box_of(e, lo, hi)) {
+          const R xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
+          const R dzl = (-a) - a * d / sl, dzu = (-c) + c * d / su;
+          ap = ratio_min(ratio_min(ap, sl, d), su, -d);
+          ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
+          s00 = s00 + (sl * a + su * c);
+          s01 = s01 + (sl * dzl + su * dzu);
+          s10 = s10 + (d * a - d * c);
+          s11 = s11 + (d * dzl - d * dzu);
+        }
+      }
+      // mu after the affine step, bilinear in (ap, ad); clamped at 0 (cancellation near the end)
+      R mua = ((s00 + ad * s01) + ap * (s10 + ad * s11)) / R(2.0 * nb);
+      if (mua < R(0)) mua = R(0);
+      const R r = mua / mu;
+      const R smu = r * r * r * mu;
+      // the corrector's linear-term shift
+      for (int e = 0; e < T; ++e) {
+        double lo, hi;
+        R hv = R(0);
+        if (box_of(e, lo, hi)) {
+          const R d = bdxa[e], xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
+          const R dzl = (-a) - a * d / sl, dzu = (-c) + c * d / su;
+          const R rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
+          const R s = a / sl + c / su;
+          hv = (-a) + c + (rl / sl - ru / su) - s * xx;
+        }
+        bh[e] = hv;
+      }
+      // corrector Newton step
+      riccati(X, xs, bsig.data(), bh.data());
+      R t = R(1);
+      for (int e = 0; e < T; ++e) {
+        double lo, hi;
+        if (!box_of(e, lo, hi)) continue;
+        const R d = sol[e] - bx[e], da = bdxa[e];
+        const R xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
+        const R dzla = (-a) - a * da / sl, dzua = (-c) + c * da / su;
+        const R rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+        const R dzl = ((-rl) - a * d) / sl, dzu = ((-ru) + c * d) / su;
+        t = ratio_min(ratio_min(t, sl, d), su, -d);
+        t = ratio_min(ratio_min(t, a, dzl), c, dzu);
+      }
+      const R al = (R(P.box_eta) * t < R(1)) ? R(P.box_eta) * t : R(1);
+      R acc2 = R(0);
+      for (int e = 0; e < T; ++e) {
+        const R d = sol[e] - bx[e], xx = bx[e];
+        double lo, hi;
+        if (box_of(e, lo, hi)) {
+          const R da = bdxa[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
+          const R dzla = (-a) - a * da / sl, dzua = (-c) + c * da / su;
+          const R rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
+          const R dzl = ((-rl) - a * d) / sl, dzu = ((-ru) + c * d) / su;
+          const R xn = xx + al * d, an = a + al * dzl, cn = c + al * dzu;
+          bx[e] = xn; bzl[e] = an; bzu[e] = cn;
+          const R sln = xn - R(lo), sun = R(hi) - xn;
+          acc2 = acc2 + (sln * an + sun * cn);
+          const R s = an / sln + cn / sun;
+          bsig[e] = s;
+          bh[e] = -(s * xn);
+        } else {
+          bx[e] = xx + al * d;
+          bsig[e] = R(0);
+          bh[e] = R(0);
+        }
+      }
+      mu = acc2 / R(2.0 * nb);
+      rfrac *= 1.0 - val(al);
+      ++it;
+      conv = val(mu) < P.box_tol && rfrac < P.box_tol;
+    }
+    for (int e = 0; e < T; ++e) sol[e] = bx[e];
+    ipm_iters = it;
+    ipm_conv = conv ? 1 : 0;
+    ipm_mu = val(mu);
   }
 
   // merit of Xn (initial-state term relative to X0)
@@ -715,8 +883,9 @@ struct Solver {
   }
 
   // returns qp_iters; alphas/steps filled
+  // box mode: ipm_it[qp] = the interior point's iterations of SQP iteration qp (may be null)
   int sqp(R* X, const R* xs, const double* goal, const double* f6, double* alphas, double* steps, int* n_alpha,
-          int* n_step) {
+          int* n_step, int* ipm_it = nullptr) {
     static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
     std::vector<R> Xn(T);
     *n_alpha = *n_step = 0;
@@ -724,6 +893,10 @@ struct Solver {
     for (qp = 0; qp < P.max_iters; ++qp) {
       linearize(X, goal, f6);
       riccati(X, xs);
+      if (P.box_mask) {
+        ipm(X, xs);
+        if (ipm_it) ipm_it[qp] = ipm_iters;
+      }
       R base = merit(X, X, goal, f6);
       double alpha = 0.0;
       for (int ai = 0; ai < 8; ++ai) {
@@ -757,20 +930,34 @@ Params make_params(int N, const double* cfg, int goal_stride) {
   P.regularize = (int)cfg[7];
   P.max_iters = (int)cfg[8];
   P.goal_stride = goal_stride;
+  P.box_mask = 0;
+  P.box_max_iters = 30;
+  P.box_tol = 1e-8; P.box_theta = 0.2; P.box_eta = 0.99; P.box_z0 = 0.1;
   return P;
+}
+// box_cfg: mask, max_iters, tol, theta, eta, z0 (BoxParams of i7m_box.h, oracle/box_ipm.py defaults)
+void set_box(Params& P, const double* box_cfg) {
+  if (!box_cfg) return;
+  P.box_mask = (int)box_cfg[0];
+  P.box_max_iters = (int)box_cfg[1];
+  P.box_tol = box_cfg[2]; P.box_theta = box_cfg[3]; P.box_eta = box_cfg[4]; P.box_z0 = box_cfg[5];
 }
 
 }  // namespace
 
 extern "C" {
 
-// Full SQP for B problems (OpenMP over problems when nthreads > 1).
-int i7m_cpu_solve(const double* model_packed, int N, const double* cfg, int B, const double* xu_in,
-                  const double* xcur, const double* goals, int goal_stride, const double* fext, double* xu_out,
-                  int* qp_iters, double* alphas, double* steps, int nthreads) {
+// Full SQP for B problems (OpenMP over problems when nthreads > 1).  box_cfg non-null with a
+// nonzero mask: config 4's box rows (ipm_iters (B, 8) per SQP iteration, and the last QP's
+// converged flag and final mu, as i7m_get_box_stats reports them; any may be null).
+int i7m_cpu_solve_box(const double* model_packed, int N, const double* cfg, const double* box_cfg, int B,
+                      const double* xu_in, const double* xcur, const double* goals, int goal_stride, const double* fext,
+                      double* xu_out, int* qp_iters, double* alphas, double* steps, int* ipm_iters, int* ipm_conv,
+                      double* ipm_mu, int nthreads) {
   if (N < 2 || N > 64 || B < 0) return -1;
   const Model M = make_model(model_packed);
-  const Params P = make_params(N, cfg, goal_stride);
+  Params P = make_params(N, cfg, goal_stride);
+  set_box(P, box_cfg);
   const int T = 18 * N - 6;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
   for (int b = 0; b < B; ++b) {
@@ -779,24 +966,37 @@ int i7m_cpu_solve(const double* model_packed, int N, const double* cfg, int B, c
     std::memcpy(X, xu_in + (size_t)b * T, sizeof(double) * T);
     int na, ns;
     qp_iters[b] = S.sqp(X, xcur + 12 * (size_t)b, goals + (size_t)b * N * goal_stride, fext ? fext + 6 * (size_t)b : nullptr,
-                        alphas + 8 * (size_t)b, steps + 8 * (size_t)b, &na, &ns);
+                        alphas + 8 * (size_t)b, steps + 8 * (size_t)b, &na, &ns,
+                        ipm_iters ? ipm_iters + 8 * (size_t)b : nullptr);
+    if (ipm_conv) ipm_conv[b] = S.ipm_conv;
+    if (ipm_mu) ipm_mu[b] = S.ipm_mu;
   }
   return 0;
 }
 
+int i7m_cpu_solve(const double* model_packed, int N, const double* cfg, int B, const double* xu_in,
+                  const double* xcur, const double* goals, int goal_stride, const double* fext, double* xu_out,
+                  int* qp_iters, double* alphas, double* steps, int nthreads) {
+  return i7m_cpu_solve_box(model_packed, N, cfg, nullptr, B, xu_in, xcur, goals, goal_stride, fext, xu_out, qp_iters,
+                           alphas, steps, nullptr, nullptr, nullptr, nthreads);
+}
+
 // Instrumented flop count of one SQP solve, split by stage:
-// out[0] linearise, out[1] QP (Riccati), out[2] line search (all merit evals actually run),
-// out[3] step/update; out[4] number of SQP iterations; out[5] merit evaluations.
-int i7m_cpu_count_flops(const double* model_packed, int N, const double* cfg, const double* xu_in, const double* xcur,
-                        const double* goal, int goal_stride, double* out) {
+// out[0] linearise, out[1] QP (Riccati; box mode: + the interior point), out[2] line search (all
+// merit evals actually run), out[3] step/update; out[4] number of SQP iterations; out[5] merit
+// evaluations; box mode (box_cfg): out[6] the interior point's flops (inside out[1]), out[7] its
+// iterations over the solve.
+int i7m_cpu_count_flops_box(const double* model_packed, int N, const double* cfg, const double* box_cfg,
+                            const double* xu_in, const double* xcur, const double* goal, int goal_stride, double* out) {
   const Model M = make_model(model_packed);
-  const Params P = make_params(N, cfg, goal_stride);
+  Params P = make_params(N, cfg, goal_stride);
+  set_box(P, box_cfg);
   const int T = 18 * N - 6;
   Solver<CountD> S(M, P);
   std::vector<CountD> X(xu_in, xu_in + T), xs(xcur, xcur + 12), Xn(T);
   static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
-  uint64_t f_lin = 0, f_qp = 0, f_ls = 0, f_step = 0;
-  int iters = 0, merits = 0;
+  uint64_t f_lin = 0, f_qp = 0, f_ls = 0, f_step = 0, f_ipm = 0;
+  int iters = 0, merits = 0, ipm_total = 0;
   for (int qp = 0; qp < P.max_iters; ++qp) {
     ++iters;
     CountD::flops = 0;
@@ -804,6 +1004,12 @@ int i7m_cpu_count_flops(const double* model_packed, int N, const double* cfg, co
     f_lin += CountD::flops;
     CountD::flops = 0;
     S.riccati(X.data(), xs.data());
+    if (P.box_mask) {
+      const uint64_t f0 = CountD::flops;
+      S.ipm(X.data(), xs.data());
+      f_ipm += CountD::flops - f0;
+      ipm_total += S.ipm_iters;
+    }
     f_qp += CountD::flops;
     CountD::flops = 0;
     CountD base = S.merit(X.data(), X.data(), goal, nullptr);
@@ -836,7 +1042,16 @@ int i7m_cpu_count_flops(const double* model_packed, int N, const double* cfg, co
   out[3] = (double)f_step;
   out[4] = iters;
   out[5] = merits;
+  if (box_cfg) {
+    out[6] = (double)f_ipm;
+    out[7] = ipm_total;
+  }
   return 0;
+}
+
+int i7m_cpu_count_flops(const double* model_packed, int N, const double* cfg, const double* xu_in, const double* xcur,
+                        const double* goal, int goal_stride, double* out) {
+  return i7m_cpu_count_flops_box(model_packed, N, cfg, nullptr, xu_in, xcur, goal, goal_stride, out);
 }
 
 }  // extern "C"

@@ -25,6 +25,9 @@ def load(path=None):
         _lib.i7m_cpu_solve.argtypes = [_DP, C.c_int, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP, _DP, _DP,
                                        C.c_int]
         _lib.i7m_cpu_count_flops.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, C.c_int, _DP]
+        _lib.i7m_cpu_solve_box.argtypes = [_DP, C.c_int, _DP, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP,
+                                           _DP, _DP, _IP, _IP, _DP, C.c_int]
+        _lib.i7m_cpu_count_flops_box.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, _DP, C.c_int, _DP]
     return _lib
 
 
@@ -57,6 +60,39 @@ def model_packed():
     return np.asarray(out, dtype=np.float64)
 
 
+def box_cfg(mask=7, max_iters=30, tol=1e-8, theta=0.2, eta=0.99, z0=0.1):
+    """Config 4's interior-point settings (oracle/box_ipm.py::ipm_box defaults, i7m_box.h BoxParams)."""
+    return np.array([mask, max_iters, tol, theta, eta, z0], dtype=np.float64)
+
+
+def solve_box(xcur, goals, XU, N, nthreads=1, fext=None, box=None, **cfg):
+    """Config 4 (box rows on q, v, u): (XU out, qp_iters, alphas, steps, ipm_iters (B, 8) per SQP
+    iteration, last QP's converged flag, last QP's mu)."""
+    lib = load()
+    XU = np.ascontiguousarray(XU, float)
+    B = XU.shape[0]
+    xcur = np.ascontiguousarray(xcur, float)
+    goals = np.ascontiguousarray(goals, float)
+    stride = goals.shape[1] // N
+    out = np.empty_like(XU)
+    qp = np.zeros(B, dtype=np.int32)
+    al = np.full((B, 8), np.nan)
+    st = np.full((B, 8), np.nan)
+    it = np.full((B, 8), -1, dtype=np.int32)
+    conv = np.zeros(B, dtype=np.int32)
+    mu = np.zeros(B)
+    f = np.ascontiguousarray(fext, float) if fext is not None else None
+    m = model_packed()
+    c = _cfg(**cfg)
+    bc = box_cfg() if box is None else np.asarray(box, float)
+    rc = lib.i7m_cpu_solve_box(_p(m), N, _p(c), _p(bc), B, _p(XU), _p(xcur), _p(goals), stride,
+                               _p(f) if f is not None else None, _p(out), qp.ctypes.data_as(_IP), _p(al), _p(st),
+                               it.ctypes.data_as(_IP), conv.ctypes.data_as(_IP), _p(mu), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("i7m_cpu_solve_box failed")
+    return out, qp, al, st, it, conv, mu
+
+
 def solve(xcur, goals, XU, N, nthreads=1, fext=None, **cfg):
     lib = load()
     XU = np.ascontiguousarray(XU, float)
@@ -78,14 +114,20 @@ def solve(xcur, goals, XU, N, nthreads=1, fext=None, **cfg):
     return out, qp, al, st
 
 
-def count_flops(xcur, goals, XU, N, **cfg):
-    """Instrumented flops of one SQP solve: dict by stage."""
+def count_flops(xcur, goals, XU, N, box=None, **cfg):
+    """Instrumented flops of one SQP solve: dict by stage (box: config 4's settings, box_cfg(),
+    adds the interior point's flops — inside "qp" — and its iterations)."""
     lib = load()
-    out = np.zeros(6)
+    out = np.zeros(8)
     m = model_packed()
     c = _cfg(**cfg)
     g = np.ascontiguousarray(goals, float)
-    lib.i7m_cpu_count_flops(_p(m), N, _p(c), _p(np.ascontiguousarray(XU, float)), _p(np.ascontiguousarray(xcur, float)),
-                            _p(g), g.shape[0] // N, _p(out))
-    return {"linearize": out[0], "qp": out[1], "linesearch": out[2], "step": out[3], "iters": out[4],
-            "merit_evals": out[5], "total": out[:4].sum()}
+    bc = None if box is None else np.asarray(box, float)
+    lib.i7m_cpu_count_flops_box(_p(m), N, _p(c), _p(bc) if bc is not None else None,
+                                _p(np.ascontiguousarray(XU, float)), _p(np.ascontiguousarray(xcur, float)),
+                                _p(g), g.shape[0] // N, _p(out))
+    d = {"linearize": out[0], "qp": out[1], "linesearch": out[2], "step": out[3], "iters": out[4],
+         "merit_evals": out[5], "total": out[:4].sum()}
+    if bc is not None:
+        d.update(ipm=out[6], ipm_iters=out[7])
+    return d

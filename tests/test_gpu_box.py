@@ -7,8 +7,11 @@ Tolerances (fp64):
       rounding differs, amplified by Sigma ~ z/s near active bounds)
   interior-point iteration counts            : identical
   full SQP with box rows                     : 1e-5 relative, alpha sequence identical
-  config 4 at full size (B=4096, N=64)       : bounds hold exactly, >= 99% converged
+  config 4 at full size (B=4096, N=64)       : bounds hold exactly, every problem converged;
+      every problem vs the C++ port: iterations and alphas identical, XU 1e-6 relative
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -102,7 +105,7 @@ def test_config4_full_size(lib, model):
     lo, hi, bm = box_ipm.box_bounds(OSQPSolverRef(N=N).P_, N)
     assert np.isfinite(out).all()
     assert (out[:, bm] >= lo[bm]).all() and (out[:, bm] <= hi[bm]).all()
-    assert conv.mean() >= 0.99, conv.mean()
+    assert conv.all(), conv.mean()  # measured: every problem converges (r03: 4096 / 4096)
     np.testing.assert_array_equal(out[:, :12], xcur)
     # two problems of the full-size batch against the oracle SQP with box rows (config 4's exact
     # size meets its oracle: same alpha sequence, 1e-5 relative)
@@ -113,3 +116,30 @@ def test_config4_full_size(lib, model):
         al = list(st["alphas"][b][: st["n_alphas"][b]])
         assert al == sq.stats["linesearch_alphas"]["values"], (b, al, sq.stats["linesearch_alphas"]["values"])
         assert _relerr(out[b], ref) <= 1e-5, (b, _relerr(out[b], ref))
+
+
+def test_config4_every_problem_matches_cpu_port(lib, model):
+    """Config 4 in full (B = 4096, N = 64, seed 46 = 42 + config index): every
+    problem against the C++ port's box mode (oracle/cpp/i7m_cpu.cpp `ipm`, itself pinned to the
+    numpy oracle by tests/test_box_oracle.py): SQP iteration counts, alpha sequences, the last
+    QP's interior-point iteration count and convergence identical for all 4096 problems; XU within
+    1e-6 relative (both solve every Newton step by a Riccati recursion; they differ by rounding,
+    amplified by Sigma ~ z / s near active bounds)."""
+    from oracle import cpu
+    from indy7_mpc_amd.synthetic import make_batch
+
+    N, B = 64, 4096
+    h = _box_handle(lib, model, N, B)
+    xcur, goals, XU = make_batch(h, model, B, N, seed=46)
+    out, st = h.solve(xcur, goals, XU)
+    it, conv, mu = h.box_stats(B)
+    ref, qp, al, _, rit, rconv, rmu = cpu.solve_box(xcur, goals, XU, N, nthreads=min(16, os.cpu_count() or 1))
+    np.testing.assert_array_equal(st["qp_iters"], qp)
+    for k in range(2):
+        sel = st["n_alphas"] > k
+        np.testing.assert_array_equal(st["alphas"][sel, k], al[sel, k])
+    np.testing.assert_array_equal(it, rit[np.arange(B), qp - 1])
+    np.testing.assert_array_equal(conv, rconv)
+    assert conv.all(), conv.mean()
+    rel = np.linalg.norm(out - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert rel.max() <= 1e-6, rel.max()

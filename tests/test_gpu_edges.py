@@ -324,6 +324,29 @@ def test_chunked_host_to_host_solve_bit_identical(lib, model, monkeypatch, chunk
     assert np.array_equal(sc, s1)
 
 
+@pytest.mark.parametrize("mode", ["box", "fused"])
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_chunked_host_to_host_box_and_fused_bit_identical(lib, model, chunks, mode):
+    """Chunked i7m_solve (default pipeline, tapered) in the two modes whose per-chunk buffers differ
+    from the split QP: config 4's box mode (the chunk's interior-point buffers through
+    bufs_at, and its box stats) and the fused pipeline (launch_fused with the chunk's offsets), each
+    against the same mode's one-piece call, bit for bit."""
+    from oracle.osqp_ref import synthetic_batch
+
+    B, N = 200, 16
+    xcur, goals, XU = synthetic_batch(B, N, seed=73)
+    kw = {"qp_mode": lib.QP_BOX} if mode == "box" else {"pipeline": lib.PIPE_FUSED}
+    h1 = lib.Handle(model, N=N, max_batch=B, h2h_chunks=1, **kw)
+    hc = lib.Handle(model, N=N, max_batch=B, h2h_chunks=chunks, **kw)
+    o1, s1 = h1.solve(xcur, goals, XU)
+    oc, sc = hc.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(oc, o1)
+    assert np.array_equal(sc, s1)
+    if mode == "box":
+        for a, b in zip(h1.box_stats(B), hc.box_stats(B)):
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("tail", ["1", "2", "3"])
 def test_split_line_search_bit_identical(lib, model, monkeypatch, tail):
     """I7M_LS_TAIL=r: the line search as two launches — r rounds of one wave per problem, then
