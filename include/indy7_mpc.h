@@ -193,6 +193,18 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
 int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals,
            int32_t goal_stride, double* sol);
 
+/* The QP's optimal cost-to-go at the first knot (the Riccati value function V~_0 in homogeneous
+ * coordinates x~ = [x_0; 1], as the backward sweep ends with it): V0 (B, 13, 13) row-major, the
+ * quadratic form the exact solve of i7m_qp minimises over the rest of the trajectory given x_0
+ * — its 12 x 12 block is d^2 J* / d x_0^2 (the sensitivity of the optimal QP cost to the initial
+ * state, the derivative of the equality multiplier of the x_0 rows l[:12] = -xs of
+ * src/osqp_solver.py:85), its last column the linear part.  Diagnostic / test hook (the reference
+ * has no counterpart; OSQP returns the multipliers `y`, src/osqp_solver.py:143).  The matrix is
+ * symmetric only to the accuracy of the recursion: returned as computed.  I7M_QP_DIRECT only,
+ * N >= 10. */
+int i7m_qp_value(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals,
+                 int32_t goal_stride, double* V0);
+
 /* I7M_QP_BOX: interior-point record of the most recent QP of problems [0, B) (the last
  * i7m_qp, or the last SQP iteration of i7m_solve): corrector steps taken, 1 if converged
  * (mu < box_tol and residuals reduced by box_tol), final mu.  Any output may be NULL. */

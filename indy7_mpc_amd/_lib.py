@@ -119,6 +119,7 @@ SIGNATURES = [
     ("i7m_solve_device", C.c_int, [_H, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                    C.c_void_p]),
     ("i7m_qp", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
+    ("i7m_qp_value", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_get_box_stats", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _DP]),
     ("i7m_linearize", C.c_int, [_H, C.c_int32, _DP, _DP, C.c_int32, _DP, _DP]),
     ("i7m_merit", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
@@ -277,6 +278,14 @@ class Handle:
         sol = np.empty_like(xu)
         _check(self._lib.i7m_qp(self._h, B, _ptr(xu), _ptr(xc), _ptr(goals), stride, _ptr(sol)))
         return sol
+
+    def qp_value(self, xu, xcur, goals):
+        """The QP's cost-to-go at the first knot, V~_0 (B, 13, 13) (i7m_qp_value): [[Vxx, vx], [vx', c]]
+        in the homogeneous coordinates [x_0; 1], as the Riccati recursion ends with it."""
+        xu, goals, B, stride, xc = self._batch(xu, goals, xcur)
+        V = np.empty((B, 13, 13))
+        _check(self._lib.i7m_qp_value(self._h, B, _ptr(xu), _ptr(xc), _ptr(goals), stride, _ptr(V)))
+        return V
 
     def box_stats(self, B):
         """Interior-point record of the last QP (box mode): (iters, converged, mu), each (B,)."""

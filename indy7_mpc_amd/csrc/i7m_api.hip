@@ -291,14 +291,17 @@ template <int ABL>
 void launch_riccati_mfma(hipStream_t s, hipEvent_t ea, hipEvent_t eb, const Bufs& W, const SolveParams& P,
                          const double* xu, const double* xs, const int* active, double* sol) {
   hipExtLaunchKernelGGL(k_riccati_mfma<ABL>, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active,
-                        W.kbuf, sol, (const double*)nullptr, (const double*)nullptr);
+                        W.kbuf, sol, (const double*)nullptr, (const double*)nullptr, (double*)nullptr);
 }
 
+// vout (i7m_qp_value): the first knot's cost-to-go V~_0 (B, 13, 13) instead of the rollout (one-wave
+// kernel only)
 int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu,
-                   const double* xs, const int* active, double* sol) {
+                   const double* xs, const int* active, double* sol, double* vout = nullptr) {
   if (P.B == 0) return I7M_OK;
   return timed(h, s, I7M_K_RICCATI, [&](hipEvent_t ea, hipEvent_t eb) {
 #ifdef I7M_DIAG
+    if (!vout) {
     // I7M_ABLATE -> ABL bits of riccati_mfma_body (diagnostic timing builds, results invalid;
     // compiled only into the -DI7M_DIAG library that tools/ load, never the shipping one)
     bool ablated = true;
@@ -314,6 +317,7 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
       default: ablated = false;
     }
     if (ablated) return;
+    }
 #endif
     // (the diag library's default path is the release selection below, so its per-wave timelines
     // show the shipping kernels)
@@ -324,7 +328,7 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
     const int bc = h->ric_bc >= 0 ? h->ric_bc
                                   : (P.B >= RIC_DPP_MIN_B ? 3 : 2) | (P.B >= RIC_PRIO_MIN_B ? 4 : 0);
     // small batches: two waves per problem (k_riccati_mfma_w2), the stage's MFMA chains split
-    const bool w2 = h->ric_w2 >= 0 ? h->ric_w2 != 0 : P.B <= RIC_W2_MAX_B;
+    const bool w2 = !vout && (h->ric_w2 >= 0 ? h->ric_w2 != 0 : P.B <= RIC_W2_MAX_B);
     if (w2) {
       auto go2 = [&](auto kern) {
         hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(128), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active,
@@ -336,7 +340,7 @@ int launch_riccati(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParam
     }
     auto go = [&](auto kern) {
       hipExtLaunchKernelGGL(kern, dim3(P.B), dim3(64), 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf,
-                            sol, (const double*)nullptr, (const double*)nullptr);
+                            sol, (const double*)nullptr, (const double*)nullptr, vout);
     };
     switch (bc) {
       case 1: go(k_riccati_mfma<0, false, 1>); break;
@@ -467,7 +471,7 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
     for (int half = 0; half < 2; ++half) {
       rc = timed(h, s, I7M_K_RICCATI_BOX, [&](hipEvent_t ea, hipEvent_t eb) {
         hipExtLaunchKernelGGL((k_riccati_mfma<0, true>), g, blk, 0, s, ea, eb, 0, P, xu, xs, W.lin, W.cost, W.qpd, W.bact, W.kbuf,
-                           sol, W.bsig, W.bh);
+                           sol, W.bsig, W.bh, (double*)nullptr);
       });
       if (rc) return rc;
       rc = timed(h, s, I7M_K_IPM, [&](hipEvent_t ea, hipEvent_t eb) {
@@ -1090,6 +1094,29 @@ int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const
   const double* qsol = nullptr;
   if ((rc = solve_qp(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol, &qsol))) return rc;
   if ((rc = copy_out(h, sol, qsol, (size_t)B * T))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_qp_value(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals, int32_t goal_stride,
+                 double* V0) {
+  int rc = check_batch(h, B, goal_stride);
+  if (rc) return rc;
+  if (B == 0) return I7M_OK;
+  if (!xu || !xcur || !goals || !V0) return fail(I7M_EINVAL, "null pointer");
+  if (h->cfg.qp_mode != I7M_QP_DIRECT) return fail(I7M_EINVAL, "i7m_qp_value: the equality-constrained QP only");
+  HIPCHK(hipSetDevice(h->dev));
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  SolveParams P = params_of(h, B, goal_stride);
+  if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
+  if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
+  if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
+  if ((rc = launch_linearize(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_goal, nullptr))) return rc;
+  // (B x 169 doubles in the solution buffer: T = 18 N - 6 >= 169 from N = 10)
+  if (T < 169) return fail(I7M_EINVAL, "i7m_qp_value needs N >= 10");
+  double* vbuf = h->d_sol;
+  if ((rc = launch_riccati(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol, vbuf))) return rc;
+  if ((rc = copy_out(h, V0, vbuf, (size_t)B * 169))) return rc;
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
 }

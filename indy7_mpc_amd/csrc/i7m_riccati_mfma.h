@@ -78,6 +78,25 @@ enum : int {
 #ifndef I7M_QXX_K0_VALU
 #define I7M_QXX_K0_VALU 1
 #endif
+#ifndef I7M_RIC_VV_PLAIN
+#define I7M_RIC_VV_PLAIN 0
+#endif
+// I7M_RIC_44X (default 0, an A/B build): Qxx's v-row k-steps and V~'s update on
+// 4x4x4_4b blocks without the homogeneous row block.  A 4x4x4_4b instruction whose B operand is a 16x16x4 B operand
+// (the layouts coincide) and whose A operand replicates one row block rb of the left factor over
+// its four block slots yields exactly register rb of the 16x16 D layout.  Rows 12..15 of Qxx and V~
+// (register 3) held only V~[12][12], the cost-to-go's constant, which no gain, x or u depends on:
+// three row blocks per k-step instead of the 16x16 MFMA's four (2 x 64 -> 6 x 16 cycles for Qxx,
+// the same for V~), A operands from LDS.  Both forms accumulate each entry's k-steps as an fma chain
+// in k order, so the results are bit-identical (tools/lib_diff.py: 0 of 4096 config-3, 0 of 256
+// config-4 problems, none of the 500 closed-loop steps).  Measured slower (profiles/r04_ric44x_ab.txt):
+// 97.9 -> 108.2 us per launch at B = 4096, 54.7 -> 67.0 at 1024, k_ipm_fused 5.43 -> 5.53 ms — the
+// twelve A-operand LDS reads per stage (the 16x16 form reads two and reuses A~'s B-operand registers
+// as Qxx's A operand), their map registers (4 VGPRs spilled at the 128 cap) and unpacking cost more
+// than the 64 fp64-pipe cycles the row blocks save.
+#ifndef I7M_RIC_44X
+#define I7M_RIC_44X 0
+#endif
 
 
 // v_mfma_f64_4x4x4_4b: four independent 4 x 4 x 4 blocks.  Lane layouts (gfx950, probed by
@@ -163,8 +182,15 @@ __device__ __forceinline__ Ric44Maps ric44_maps(const int l) {
   // only to the accuracy of K~ = -H^-1 G~, and H can be very ill-conditioned (R = 1e-5 w against
   // Bu' V Bu), so H = Bu' (V~')_vv Bu keeps the recursion on the one matrix V~' throughout — with
   // V~_vv instead, 1e-8 relative errors at N = 32 and 1e-4 at N = 64 (measured).
+  // (-DI7M_RIC_VV_PLAIN=1, a test build only: V~_vv un-transposed, the recursion that loses accuracy
+  // — tests/test_gpu_riccati_value.py fails on it)
+#if I7M_RIC_VV_PLAIN
+  M.vvS = pk16((lq >= 2 && lr >= 6 && lr < 12) ? MO_VV + 6 * (lq - 2) + (lr - 6) : sink,
+               (lr >= 6 && lr < 12) ? MO_VV + 6 * (lq + 2) + (lr - 6) : sink);
+#else
   M.vvS = pk16((lq >= 2 && lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq - 2) : sink,
                (lr >= 6 && lr < 12) ? MO_VV + 6 * (lr - 6) + (lq + 2) : sink);
+#endif
   M.w0S = pk16((lq >= 2 && lr < 13) ? MO_W0V + 13 * (lq - 2) + lr : sink, (lr < 13) ? MO_W0V + 13 * (lq + 2) + lr : sink);
   return M;
 }
@@ -214,6 +240,9 @@ __device__ __forceinline__ void ric44_g(const Ric44Maps& M, double* __restrict__
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ double mfma44_nb(double a, double b, double c) {  // a (-b) + c, 4x4x4_4b
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 2);
 }
 __device__ __forceinline__ d4 mfma_nb(double a, double b, d4 c) {  // a (-b) + c
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 2);
@@ -469,7 +498,8 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
                                                   double* __restrict__ kbuf, double* __restrict__ sol,
                                                   const double* __restrict__ bsig, const double* __restrict__ bh,
                                                   double* __restrict__ sh, const int l,
-                                                  double* __restrict__ hinv = nullptr, const bool kff_only = false) {
+                                                  double* __restrict__ hinv = nullptr, const bool kff_only = false,
+                                                  double* __restrict__ vout = nullptr) {
   static_assert(!W2 || (!BOX && !HINV && ABL == 0), "two-wave body: plain QP only");
   const int lr = l & 15, lq = l >> 4;
   const int N = P.N;
@@ -545,6 +575,26 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
   // the C inputs); not the two-wave kernel (see I7M_RIC_44) nor the diagnostic LDS-exchange elimination
   constexpr bool S44 = I7M_RIC_44 && !(ABL & 4) && !W2;
   Ric44Maps M44 = ric44_maps<BOX>(l);
+  // I7M_RIC_44X: A operands of the row-block products (lane l: k = l >> 4, row i = l & 3 of the block)
+  //   Qxx: A~'[4rb + i][4ks + k] = A~[4ks + k][4rb + i], k-steps ks = 1, 2 (packed lo | hi)
+  //   V~ : K~'[4rb + i][4ks + k] = K~[4ks + k][4rb + i], k-steps ks = 0, 1
+  constexpr bool X44 = I7M_RIC_44X && S44;
+  unsigned qxA[3], vxA[3];
+#pragma unroll
+  for (int rb = 0; rb < 3; ++rb) {
+    const int k = l >> 4, c = 4 * rb + (l & 3);
+    int a[2];
+#pragma unroll
+    for (int ks = 1; ks < 3; ++ks) {
+      const int r = 4 * ks + k;
+      int o = MO_ZERO;
+      if (r < 6) o = (c == r) ? MO_ONE : (c == r + 6 ? MO_DT : MO_ZERO);
+      else o = c < 6 ? MO_AQ + 6 * (r - 6) + c : MO_AV + 6 * (r - 6) + (c - 6);
+      a[ks - 1] = o;
+    }
+    qxA[rb] = pk16(a[0], a[1]);
+    vxA[rb] = pk16(MO_KT + 13 * k + c, k < 2 ? MO_KT + 13 * (4 + k) + c : MO_ZERO);
+  }
   constexpr int SE = BOX ? 176 : 140;  // stash length
   // Branch-free lane-conditional stores (lanes with nothing to store write a per-lane sink slot,
   // DESIGN.md §7) in the plain QP only: in the box body (k_ipm_fused) the sink addresses and
@@ -773,7 +823,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     d4 W0;
     // (lr == 12 ? V : +0) as one fma per register instead of two 32-bit selects
 #pragma unroll
-    for (int i = 0; i < 4; ++i) W0[i] = fma(V[i], m12, 0.0);
+    for (int i = 0; i < 4; ++i) W0[i] = (X44 && i == 3) ? 0.0 : fma(V[i], m12, 0.0);
 #pragma unroll
     for (int s = 0; s < 3; ++s) W0 = mfma(V[s], bA[s], W0);
     if (ABL & 512) tb = tstamp(W0[0] + W0[1] + W0[2] + W0[3]);
@@ -785,7 +835,7 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       sh[lo16(M44.w0S)] = W0[1];
       sh[hi16(M44.w0S)] = W0[2];
       ric44_h<BOX>(M44, sh);
-      Z00[3] = fma(W0[3], mlq0, Z00[3]);  // row 12's k-step: + W0[12][:] on the lanes lq == 0
+      if (!X44) Z00[3] = fma(W0[3], mlq0, Z00[3]);  // row 12's k-step: + W0[12][:] on the lanes lq == 0
       if constexpr (I7M_QXX_K0_VALU) {
         // k-step 0 (A~'s q rows 0..3: 1 at (k, k), dt at (k, k + 6)) on the VALU: rows 0..3 of Qxx
         // gain W0's rows 0..3 (same lanes), rows 6..9 dt times them (the other half of the wave:
@@ -806,8 +856,17 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
         // product changes 4 091 of 4 096 config-3 solves, the fma none)
         Z00[1] = fma(up, mdt_hi, Z00[1]);  // rows 6, 7 (lq 2, 3)
         Z00[2] = fma(dn, mdt_lo, Z00[2]);  // rows 8, 9 (lq 0, 1)
+        if constexpr (X44) {
+          // k-steps 1, 2 as three row blocks each (the 16x16 D registers 0..2)
 #pragma unroll
-        for (int s = 1; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+          for (int rb = 0; rb < 3; ++rb) {
+            Z00[rb] = mfma44(sh[lo16(qxA[rb])], W0[1], Z00[rb]);
+            Z00[rb] = mfma44(sh[hi16(qxA[rb])], W0[2], Z00[rb]);
+          }
+        } else {
+#pragma unroll
+          for (int s = 1; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
+        }
       } else {
 #pragma unroll
         for (int s = 0; s < 3; ++s) Z00 = mfma(bA[s], W0[s], Z00);
@@ -946,7 +1005,13 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
       }
       wave_sync();
       if (ABL & 512) tm3 = tstamp(E[0]);
-      if constexpr (S44) {  // Z10 holds -G~ (ric44_g)
+      if constexpr (X44) {  // Z10 holds -G~ (ric44_g); row blocks 0..2 of V~
+#pragma unroll
+        for (int rb = 0; rb < 3; ++rb) {
+          V[rb] = mfma44_nb(sh[lo16(vxA[rb])], Z10[0], Z00[rb]);
+          V[rb] = mfma44_nb(sh[hi16(vxA[rb])], Z10[1], V[rb]);
+        }
+      } else if constexpr (S44) {  // Z10 holds -G~ (ric44_g)
         V = mfma_nb(sh[oK[0]], Z10[0], Z00);
         V = mfma_nb(sh[oK[1]], Z10[1], V);
       } else {
@@ -981,6 +1046,23 @@ __device__ __forceinline__ void riccati_mfma_body(const int b, const SolveParams
     }
   }
 
+  if constexpr (!W2 && !BOX) {
+    // i7m_qp_value: the cost-to-go of the first knot, V~_0 (13 x 13, as the accumulators hold it:
+    // lane l register i = row lq + 4i, column lr), instead of the rollout (vout wave-uniform)
+    if (vout) {
+      // rows 0..11 as held (I7M_RIC_44X: row 12 is not formed; it is filled from column 12, and the
+      // constant V~[12][12], which nothing depends on, is NaN)
+      double* o = vout + (long)b * 169;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = lq + 4 * i;
+        if (lr < 13) o[13 * r + lr] = V[i];
+        if (lr == 12) o[13 * 12 + r] = V[i];
+      }
+      if (l == 12) o[168] = X44 ? __builtin_nan("") : V[3];
+      return;
+    }
+  }
   if (W2) {
     lds_sync();  // wave 1's last reads of the stage LDS before the rollout reuses it
     if (w != 0) return;
@@ -1147,13 +1229,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
                                                      const int* __restrict__ active,
                                                      double* __restrict__ kbuf, double* __restrict__ sol,
                                                      const double* __restrict__ bsig = nullptr,
-                                                     const double* __restrict__ bh = nullptr) {
+                                                     const double* __restrict__ bh = nullptr,
+                                                     double* __restrict__ vout = nullptr) {
   I7M_TL(2);
   const int b = blockIdx.x;
   if (b >= P.B) return;
   if (active && !active[b]) return;
   __shared__ double sh[MO_TOTAL];
-  riccati_mfma_body<ABL, BOX, false, BC>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, bsig, bh, sh, threadIdx.x);
+  riccati_mfma_body<ABL, BOX, false, BC>(b, P, xu, xs, lin, cost, qpd, kbuf, sol, bsig, bh, sh, threadIdx.x, nullptr,
+                                         false, vout);
 }
 
 }  // namespace i7m
