@@ -235,7 +235,9 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
             "qp_iters_agreement": float((st["qp_iters"] == qp).mean()),
             "ipm_iters_agreement": float((it == rit[np.arange(B), qp - 1]).mean()),
             "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
-            "reference": "oracle/cpp/i7m_cpu.cpp box mode (oracle/box_ipm.py restated, Riccati Newton steps)"}
+            "reference": "oracle/cpp/i7m_cpu.cpp box mode (oracle/box_ipm.py restated, Riccati Newton steps)",
+            "gate": "SQP and interior-point iteration counts and alphas identical; XU median <= 1e-6, max <= 1e-3 "
+                    "(the interior point resolves XU only to ~1e-4 at tol 1e-8: oracle/studies/box_sensitivity.py)"}
         # CPU baseline: a bounded sample of the same draws, 1 thread and the job's share
         t0 = time.perf_counter()
         cpu.solve_box(xcur[:4], goals[:4], XU[:4], N, nthreads=1)
