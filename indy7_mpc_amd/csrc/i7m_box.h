@@ -106,6 +106,12 @@ __device__ __forceinline__ int wave_isum(int v) {
 __device__ __forceinline__ double ratio_min(double t, double v, double dv) {
   return (dv < 0.0) ? fmin(t, -v / dv) : t;
 }
+// both primal tests of a bounded entry (s_l + t d >= 0, s_u - t d >= 0): at most one binds, so one
+// division — (-s_l) / d for d < 0, s_u / d for d > 0, the same values ratio_min gives bit for bit
+__device__ __forceinline__ double ratio_min_box(double t, double sl, double su, double d) {
+  const double q = ((d < 0.0) ? -sl : su) / d;
+  return (d != 0.0) ? fmin(t, q) : t;
+}
 
 // The three phases of one interior-point iteration, as wave-level device functions of problem
 // b (one wavefront; every lane ends with the same IpmState, reductions are xor-shuffle trees).
@@ -127,11 +133,11 @@ __device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveP
     if (box_of(Bt, e, lo, hi)) {
       const double w = hi - lo;
       xv = fmin(fmax(xv, lo + BP.theta * w), hi - BP.theta * w);
-      const double sl = xv - lo, su = hi - xv;
-      a = BP.z0 / sl;
-      c = BP.z0 / su;
+      const double sl = xv - lo, su = hi - xv, isl = 1.0 / sl, isu = 1.0 / su;
+      a = BP.z0 * isl;
+      c = BP.z0 * isu;
       acc += sl * a + su * c;
-      s = a / sl + c / su;
+      s = a * isl + c * isu;
       ++nb;
     }
     x[o + e] = xv;
@@ -155,6 +161,10 @@ __device__ __forceinline__ IpmState ipm_init_body(const BoxTab& Bt, const SolveP
 
 // Predictor: dx_aff = y - x; affine step lengths and mu_aff (one pass); sigma*mu (-> S.smu);
 // the corrector's h (a second pass).
+// Every element term divides by the slacks through their reciprocals 1 / s_l, 1 / s_u, formed once
+// per element and pass (oracle/box_ipm.py and the C++ port form them the same way): 26 IEEE
+// divisions per bounded entry and iteration became 16 (the ratio tests keep theirs, and the two
+// primal tests share one).
 // Element passes run in chunks of IPM_U elements per lane: the chunk's operands are all loaded
 // (clamped addresses, no branches) before any is used, so one wave has IPM_U x (2..5) loads in
 // flight instead of waiting out the memory latency element by element.  The per-lane order of
@@ -198,8 +208,9 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
         double lo, hi;
         if (box_of(Bt, e, lo, hi)) {
           const double xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
-          const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
-          ap = ratio_min(ratio_min(ap, sl, d), su, -d);
+          const double isl = 1.0 / sl, isu = 1.0 / su;
+          const double dzl = -a - a * d * isl, dzu = -c + c * d * isu;
+          ap = ratio_min_box(ap, sl, su, d);
           ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
           s00 += sl * a + su * c;
           s01 += sl * dzl + su * dzu;
@@ -237,10 +248,11 @@ __device__ __forceinline__ void ipm_pred_body(const BoxTab& Bt, const SolveParam
         double lo, hi, hv = 0.0;
         if (box_of(Bt, e, lo, hi)) {
           const double d = dv[u], xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
-          const double dzl = -a - a * d / sl, dzu = -c + c * d / su;
+          const double isl = 1.0 / sl, isu = 1.0 / su;
+          const double dzl = -a - a * d * isl, dzu = -c + c * d * isu;
           const double rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
-          const double s = a / sl + c / su;
-          hv = -a + c + (rl / sl - ru / su) - s * xx;
+          const double s = a * isl + c * isu;
+          hv = -a + c + (rl * isl - ru * isu) - s * xx;
         }
         if (dh) dh[o + e] = hv - hold[u];  // the corrector's change of the linear terms
         h[o + e] = hv;
@@ -280,10 +292,11 @@ __device__ __forceinline__ void ipm_corr_body(const BoxTab& Bt, const SolveParam
       if (e < T && box_of(Bt, e, lo, hi)) {
         const double d = yv[u] - xv[u], da = dav[u];
         const double xx = xv[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
-        const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+        const double isl = 1.0 / sl, isu = 1.0 / su;
+        const double dzla = -a - a * da * isl, dzua = -c + c * da * isu;
         const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-        const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
-        t = ratio_min(ratio_min(t, sl, d), su, -d);
+        const double dzl = (-rl - a * d) * isl, dzu = (-ru + c * d) * isu;
+        t = ratio_min_box(t, sl, su, d);
         t = ratio_min(ratio_min(t, a, dzl), c, dzu);
       }
     }
@@ -311,16 +324,17 @@ __device__ __forceinline__ void ipm_corr_body(const BoxTab& Bt, const SolveParam
         double lo, hi;
         if (box_of(Bt, e, lo, hi)) {
           const double da = dav[u], sl = xx - lo, su = hi - xx, a = av[u], c = cv[u];
-          const double dzla = -a - a * da / sl, dzua = -c + c * da / su;
+          const double isl = 1.0 / sl, isu = 1.0 / su;
+          const double dzla = -a - a * da * isl, dzua = -c + c * da * isu;
           const double rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-          const double dzl = (-rl - a * d) / sl, dzu = (-ru + c * d) / su;
+          const double dzl = (-rl - a * d) * isl, dzu = (-ru + c * d) * isu;
           const double xn = xx + al * d, an = a + al * dzl, cn = c + al * dzu;
           x[o + e] = xn;
           zl[o + e] = an;
           zu[o + e] = cn;
           const double sln = xn - lo, sun = hi - xn;
           acc += sln * an + sun * cn;
-          const double s = an / sln + cn / sun;
+          const double s = an * (1.0 / sln) + cn * (1.0 / sun);
           sig[o + e] = s;
           h[o + e] = -s * xn;
         } else {

@@ -16,12 +16,24 @@
 
 namespace i7m {
 
-// the cold path, kept out of line so the library code is not inlined at every call site
-__host__ __device__ __noinline__ void sincos_lib(double x, double* sp, double* cp) { sincos(x, sp, cp); }
+// the cold path, kept out of line so the library code is not inlined at every call site.  It
+// returns its pair by value: passing the caller's output pointers to an out-of-line call takes the
+// addresses of the callers' sin / cos arrays, which then live in scratch memory on the hot path too
+// (k_linesearch stored and re-loaded all twelve values of a knot's evaluation through scratch).
+struct SinCos {
+  double s, c;
+};
+__host__ __device__ __noinline__ SinCos sincos_lib(double x) {
+  SinCos r;
+  sincos(x, &r.s, &r.c);
+  return r;
+}
 
 __host__ __device__ __forceinline__ void sincos_q(double x, double* sp, double* cp) {
   if (!(fabs(x) < 1048576.0)) {  // also NaN / inf
-    sincos_lib(x, sp, cp);
+    const SinCos r = sincos_lib(x);
+    *sp = r.s;
+    *cp = r.c;
     return;
   }
   const double n = rint(x * 0.6366197723675814);  // 2 / pi

@@ -91,8 +91,10 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
         return IPMResult(x, np.zeros(n), np.zeros(n), 0, True)
     w = np.where(bm, hi - lo, 0.0)
     x[bm] = np.clip(x_eq[bm], (lo + theta * w)[bm], (hi - theta * w)[bm])
-    zl = np.where(bm, z0 / np.where(bm, x - lo, 1.0), 0.0)
-    zu = np.where(bm, z0 / np.where(bm, hi - x, 1.0), 0.0)
+    # (every term divides by the slacks through their reciprocals, formed once per pass — as the
+    # GPU's i7m_box.h and the C++ port do)
+    zl = np.where(bm, z0 * (1.0 / np.where(bm, x - lo, 1.0)), 0.0)
+    zu = np.where(bm, z0 * (1.0 / np.where(bm, hi - x, 1.0)), 0.0)
     K0 = bmat([[Pf, A.T], [A, None]], format="csc")
     res = IPMResult(x, zl, zu, 0, False)
     rfrac = 1.0
@@ -105,7 +107,8 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
         if mu < tol and rfrac < tol:
             res.converged = True
             break
-        sig = np.where(bm, zl / sl + zu / su, 0.0)
+        isl, isu = 1.0 / sl, 1.0 / su
+        sig = np.where(bm, zl * isl + zu * isu, 0.0)
         K = (K0 + bmat([[diags(sig), None], [None, csc_matrix((A.shape[0], A.shape[0]))]])).tocsc()
         lu = splu(K)
 
@@ -114,8 +117,8 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
 
         # predictor (tau = 0)
         dxa = newton(g - sig * x)
-        dzla = np.where(bm, -zl - zl * dxa / sl, 0.0)
-        dzua = np.where(bm, -zu + zu * dxa / su, 0.0)
+        dzla = np.where(bm, -zl - zl * dxa * isl, 0.0)
+        dzua = np.where(bm, -zu + zu * dxa * isu, 0.0)
         ap = min(_ratio(sl, dxa, bm), _ratio(su, -dxa, bm))
         ad = min(_ratio(zl, dzla, bm), _ratio(zu, dzua, bm))
         # the complementarity after the affine step is bilinear in (ap, ad): four sums
@@ -135,10 +138,10 @@ def ipm_box(Pf, g, A, b, x_eq, lo, hi, bm, tol=1e-8, max_iters=30, theta=0.2, et
         # corrector
         rl = np.where(bm, sl * zl + dxa * dzla - smu, 0.0)
         ru = np.where(bm, su * zu - dxa * dzua - smu, 0.0)
-        ell = g - zl + zu + np.where(bm, rl / sl - ru / su, 0.0) - sig * x
+        ell = g - zl + zu + np.where(bm, rl * isl - ru * isu, 0.0) - sig * x
         dx = newton(ell)
-        dzl = np.where(bm, (-rl - zl * dx) / sl, 0.0)
-        dzu = np.where(bm, (-ru + zu * dx) / su, 0.0)
+        dzl = np.where(bm, (-rl - zl * dx) * isl, 0.0)
+        dzu = np.where(bm, (-ru + zu * dx) * isu, 0.0)
         a = min(_ratio(sl, dx, bm), _ratio(su, -dx, bm), _ratio(zl, dzl, bm), _ratio(zu, dzu, bm))
         a = min(1.0, eta * a)
         res.alpha.append(a)

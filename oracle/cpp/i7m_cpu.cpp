@@ -745,11 +745,11 @@ struct Solver {
         const double l1 = lo + theta * w, h1 = hi - theta * w;
         if (xv < R(l1)) xv = R(l1);
         if (R(h1) < xv) xv = R(h1);
-        const R sl = xv - R(lo), su = R(hi) - xv;
-        a = R(z0) / sl;
-        c = R(z0) / su;
+        const R sl = xv - R(lo), su = R(hi) - xv, isl = R(1) / sl, isu = R(1) / su;
+        a = R(z0) * isl;
+        c = R(z0) * isu;
         acc = acc + (sl * a + su * c);
-        s = a / sl + c / su;
+        s = a * isl + c * isu;
         ++nb;
       }
       bx[e] = xv; bzl[e] = a; bzu[e] = c; bsig[e] = s;
@@ -769,7 +769,8 @@ struct Solver {
         double lo, hi;
         if (box_of(e, lo, hi)) {
           const R xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
-          const R dzl = (-a) - a * d / sl, dzu = (-c) + c * d / su;
+          const R isl = R(1) / sl, isu = R(1) / su;
+          const R dzl = (-a) - a * d * isl, dzu = (-c) + c * d * isu;
           ap = ratio_min(ratio_min(ap, sl, d), su, -d);
           ad = ratio_min(ratio_min(ad, a, dzl), c, dzu);
           s00 = s00 + (sl * a + su * c);
@@ -789,10 +790,11 @@ struct Solver {
         R hv = R(0);
         if (box_of(e, lo, hi)) {
           const R d = bdxa[e], xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
-          const R dzl = (-a) - a * d / sl, dzu = (-c) + c * d / su;
+          const R isl = R(1) / sl, isu = R(1) / su;
+          const R dzl = (-a) - a * d * isl, dzu = (-c) + c * d * isu;
           const R rl = sl * a + d * dzl - smu, ru = su * c - d * dzu - smu;
-          const R s = a / sl + c / su;
-          hv = (-a) + c + (rl / sl - ru / su) - s * xx;
+          const R s = a * isl + c * isu;
+          hv = (-a) + c + (rl * isl - ru * isu) - s * xx;
         }
         bh[e] = hv;
       }
@@ -804,9 +806,10 @@ struct Solver {
         if (!box_of(e, lo, hi)) continue;
         const R d = sol[e] - bx[e], da = bdxa[e];
         const R xx = bx[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
-        const R dzla = (-a) - a * da / sl, dzua = (-c) + c * da / su;
+        const R isl = R(1) / sl, isu = R(1) / su;
+        const R dzla = (-a) - a * da * isl, dzua = (-c) + c * da * isu;
         const R rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-        const R dzl = ((-rl) - a * d) / sl, dzu = ((-ru) + c * d) / su;
+        const R dzl = ((-rl) - a * d) * isl, dzu = ((-ru) + c * d) * isu;
         t = ratio_min(ratio_min(t, sl, d), su, -d);
         t = ratio_min(ratio_min(t, a, dzl), c, dzu);
       }
@@ -817,14 +820,15 @@ struct Solver {
         double lo, hi;
         if (box_of(e, lo, hi)) {
           const R da = bdxa[e], sl = xx - R(lo), su = R(hi) - xx, a = bzl[e], c = bzu[e];
-          const R dzla = (-a) - a * da / sl, dzua = (-c) + c * da / su;
+          const R isl = R(1) / sl, isu = R(1) / su;
+          const R dzla = (-a) - a * da * isl, dzua = (-c) + c * da * isu;
           const R rl = sl * a + da * dzla - smu, ru = su * c - da * dzua - smu;
-          const R dzl = ((-rl) - a * d) / sl, dzu = ((-ru) + c * d) / su;
+          const R dzl = ((-rl) - a * d) * isl, dzu = ((-ru) + c * d) * isu;
           const R xn = xx + al * d, an = a + al * dzl, cn = c + al * dzu;
           bx[e] = xn; bzl[e] = an; bzu[e] = cn;
           const R sln = xn - R(lo), sun = R(hi) - xn;
           acc2 = acc2 + (sln * an + sun * cn);
-          const R s = an / sln + cn / sun;
+          const R s = an * (R(1) / sln) + cn * (R(1) / sun);
           bsig[e] = s;
           bh[e] = -(s * xn);
         } else {

@@ -119,8 +119,10 @@ def test_config4_full_size(lib, model):
         assert _relerr(out[b], ref) <= 1e-5, (b, _relerr(out[b], ref))
 
 
-def test_config4_every_problem_matches_cpu_port(lib, model):
-    """Config 4 in full (B = 4096, N = 64, seed 46 = 42 + config index): every
+@pytest.mark.parametrize("N,B,seed", [(64, 4096, 46), (32, 1024, 146), (16, 256, 246)])
+def test_config4_every_problem_matches_cpu_port(lib, model, N, B, seed):
+    """Config 4 in full (B = 4096, N = 64, seed 46 = 42 + config index), and the box mode
+    at N = 32 (B = 1024) and N = 16 (B = 256): every
     problem against the C++ port's box mode (oracle/cpp/i7m_cpu.cpp `ipm`, itself pinned to the
     numpy oracle by tests/test_box_oracle.py): SQP iteration counts, alpha sequences, the last
     QP's interior-point iteration count and convergence identical for all 4096 problems.  XU: median
@@ -133,9 +135,8 @@ def test_config4_every_problem_matches_cpu_port(lib, model):
     from oracle import cpu
     from indy7_mpc_amd.synthetic import make_batch
 
-    N, B = 64, 4096
     h = _box_handle(lib, model, N, B)
-    xcur, goals, XU = make_batch(h, model, B, N, seed=46)
+    xcur, goals, XU = make_batch(h, model, B, N, seed=seed)
     out, st = h.solve(xcur, goals, XU)
     it, conv, mu = h.box_stats(B)
     ref, qp, al, _, rit, rconv, rmu = cpu.solve_box(xcur, goals, XU, N, nthreads=min(16, os.cpu_count() or 1))
