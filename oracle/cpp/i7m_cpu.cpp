@@ -18,6 +18,7 @@
 //   ipm (box_mask != 0)              config 4's box rows (no reference
 //                                    counterpart): oracle/box_ipm.py::ipm_box, Newton steps by
 //                                    riccati with the (Sigma, h) shifts, as i7m_box.h on the GPU
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -323,6 +324,12 @@ struct Params {
   // config 4 box rows (oracle/box_ipm.py; 0 = the reference's equality-only QP)
   int box_mask, box_max_iters;
   double box_tol, box_theta, box_eta, box_z0;
+};
+
+// ADMM mode settings (OSQP's defaults; oracle/osqp_admm.py DEFAULTS)
+struct AdmmParams {
+  double rho0 = 0.1, sigma = 1e-6, alpha = 1.6, eps_abs = 1e-3, eps_rel = 1e-3, adapt_tol = 5.0;
+  int max_iter = 4000, check = 25, scaling = 10, gap = 1, adapt_interval = 0;
 };
 
 template <class R>
@@ -886,17 +893,418 @@ struct Solver {
     return qc + vc + uc + R(P.mu) * cv;
   }
 
+  // ---- ADMM mode: OSQP's algorithm (oracle/osqp_admm.py, which reproduces the reference's
+  // printed closed loop) in the block form the GPU's k_admm runs (indy7_mpc_amd/csrc/i7m_admm.h):
+  // Ruiz scaling in place on the per-stage blocks, the x-update by a block Cholesky of the
+  // reduced matrix M = P + sigma I + A' diag(rho) A (block tridiagonal: 18 x 18 diagonal blocks,
+  // 12 x 18 couplings), kept as explicit inverses Linv_k of the diagonal factors and the coupling
+  // blocks C_k, so that every solve is mat-vecs.  A's rows are the reference's (src/osqp_solver.py:
+  // 54-68, 83-101): block 0 = -x_0, block k+1 = J_k z_k - x_{k+1} with J_k = [[I, dt I, 0],
+  // [Aq, Av, Bu]]; l = u = [-xs; -(0, cv_k)].  The iterates live in the caller's state (scaled,
+  // as OSQP keeps them between solves: the reference's solver object, src/osqp_solver.py:38-40).
+  struct AdmmState {
+    double *x, *z, *y, *qold, *rho;  // T, m, m, T, 1 (scaled x, z, y; the previous QP's q; rho)
+  };
+  AdmmParams A_;
+  int admm_it = 0, admm_solved = 0;
+  // per-stage scaled data (in place, as OSQP's scale_data multiplies its stored matrices)
+  std::vector<double> aPq, aPd, aJ, aI, aqs, als, aD, aE, aLinv, aC;
+  double ac = 1.0;
+
+  static double limit_sc(double v) { return v < 1e-4 ? 1.0 : (v > 1e4 ? 1e4 : v); }
+
+  void admm_alloc() {
+    const int N = P.N, m = 12 * N;
+    aPq.assign(36 * N, 0.0); aPd.assign(T, 0.0); aJ.assign(216 * (N - 1), 0.0); aI.assign(m, 0.0);
+    aqs.assign(T, 0.0); als.assign(m, 0.0); aD.assign(T, 1.0); aE.assign(m, 1.0);
+    aLinv.assign(324 * N, 0.0); aC.assign(216 * (N - 1), 0.0);
+  }
+
+  // unscaled data of the QP at X (after linearize): P blocks, J_k, the -I entries, l; then the
+  // Ruiz passes with the previous QP's q (OSQP re-scales inside update(Ax), before update(q)).
+  void admm_setup(const R* X, const R* xs, const double* qold) {
+    const int N = P.N, m = 12 * N;
+    for (int k = 0; k < N; ++k) {
+      const R* w = &cost[10 * k];
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) aPq[36 * k + 6 * i + j] = val(w[6] * (w[i] * w[j]));
+      for (int i = 0; i < 6; ++i) aPd[18 * k + i] = 0.0;  // the q diagonal lives in aPq
+      for (int i = 6; i < 12; ++i) aPd[18 * k + i] = val(w[7]);
+      if (k < N - 1)
+        for (int i = 12; i < 18; ++i) aPd[18 * k + i] = val(w[8]);
+    }
+    for (int k = 0; k + 1 < N; ++k) {
+      const R* L = &lin[114 * k];
+      double* G = &aJ[216 * k];
+      for (int i = 0; i < 12; ++i)
+        for (int j = 0; j < 18; ++j) {
+          double v;
+          if (i < 6) v = (j == i) ? 1.0 : (j == 6 + i ? P.dt : 0.0);
+          else if (j < 6) v = val(L[6 * (i - 6) + j]);
+          else if (j < 12) v = val(L[36 + 6 * (i - 6) + j - 6]);
+          else v = val(L[72 + 6 * (i - 6) + j - 12]);
+          G[18 * i + j] = v;
+        }
+      // l of block k+1: -(x_next - J_k z_k) with the q rows' offset exactly 0
+      const R* x = X + 18 * k;
+      for (int i = 0; i < 6; ++i) {
+        R acc = R(0);
+        for (int j = 0; j < 6; ++j) acc = acc + L[6 * i + j] * x[j] + L[36 + 6 * i + j] * x[6 + j] + L[72 + 6 * i + j] * x[12 + j];
+        const R cv = (x[6 + i] + L[108 + i] * R(P.dt)) - acc;
+        als[12 * (k + 1) + i] = 0.0;
+        als[12 * (k + 1) + 6 + i] = -val(cv);
+      }
+    }
+    for (int i = 0; i < 12; ++i) als[i] = -val(xs[i]);
+    for (int r = 0; r < m; ++r) aI[r] = -1.0;
+    for (int e = 0; e < T; ++e) { aqs[e] = qold[e]; aD[e] = 1.0; }
+    for (int r = 0; r < m; ++r) aE[r] = 1.0;
+    ac = 1.0;
+    std::vector<double> Dt(T), Et(m);
+    for (int pass = 0; pass < A_.scaling; ++pass) {
+      // column inf-norms of [P; A] and row inf-norms of A (OSQP compute_inf_norm_cols_KKT)
+      for (int e = 0; e < T; ++e) Dt[e] = 0.0;
+      for (int r = 0; r < m; ++r) Et[r] = 0.0;
+      admm_colP(Dt.data());
+      for (int r = 0; r < m; ++r) {
+        const int col = 18 * (r / 12) + r % 12;
+        const double a = std::fabs(aI[r]);
+        Dt[col] = std::max(Dt[col], a);
+        Et[r] = std::max(Et[r], a);
+      }
+      for (int k = 0; k + 1 < N; ++k)
+        for (int i = 0; i < 12; ++i)
+          for (int j = 0; j < 18; ++j) {
+            const double a = std::fabs(aJ[216 * k + 18 * i + j]);
+            Dt[18 * k + j] = std::max(Dt[18 * k + j], a);
+            Et[12 * (k + 1) + i] = std::max(Et[12 * (k + 1) + i], a);
+          }
+      for (int e = 0; e < T; ++e) Dt[e] = 1.0 / std::sqrt(limit_sc(Dt[e]));
+      for (int r = 0; r < m; ++r) Et[r] = 1.0 / std::sqrt(limit_sc(Et[r]));
+      // P <- D P D, A <- E A D, q <- D q (row factor first, as mat_premult_diag then postmult)
+      for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < 6; ++i)
+          for (int j = i; j < 6; ++j) {
+            const double v = aPq[36 * k + 6 * i + j] * Dt[18 * k + i] * Dt[18 * k + j];
+            aPq[36 * k + 6 * i + j] = aPq[36 * k + 6 * j + i] = v;
+          }
+        const int hi = k < N - 1 ? 18 : 12;
+        for (int i = 6; i < hi; ++i) aPd[18 * k + i] = aPd[18 * k + i] * Dt[18 * k + i] * Dt[18 * k + i];
+      }
+      for (int r = 0; r < m; ++r) aI[r] = aI[r] * Et[r] * Dt[18 * (r / 12) + r % 12];
+      for (int k = 0; k + 1 < N; ++k)
+        for (int i = 0; i < 12; ++i)
+          for (int j = 0; j < 18; ++j) aJ[216 * k + 18 * i + j] = aJ[216 * k + 18 * i + j] * Et[12 * (k + 1) + i] * Dt[18 * k + j];
+      for (int e = 0; e < T; ++e) { aqs[e] = Dt[e] * aqs[e]; aD[e] = aD[e] * Dt[e]; }
+      for (int r = 0; r < m; ++r) aE[r] = aE[r] * Et[r];
+      // cost normalisation
+      for (int e = 0; e < T; ++e) Dt[e] = 0.0;
+      admm_colP(Dt.data());
+      double mean = 0.0;
+      for (int e = 0; e < T; ++e) mean += Dt[e];
+      mean /= T;
+      double qn = 0.0;
+      for (int e = 0; e < T; ++e) qn = std::max(qn, std::fabs(aqs[e]));
+      qn = limit_sc(qn);
+      double ct = 1.0 / limit_sc(std::max(mean, qn));
+      for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < 36; ++i) aPq[36 * k + i] *= ct;
+        const int hi = k < N - 1 ? 18 : 12;
+        for (int i = 6; i < hi; ++i) aPd[18 * k + i] *= ct;
+      }
+      for (int e = 0; e < T; ++e) aqs[e] *= ct;
+      ac *= ct;
+    }
+    for (int r = 0; r < m; ++r) als[r] = aE[r] * als[r];
+  }
+  // max(|P_s| column) into out (symmetric P: the q block's full columns, the v / u diagonals)
+  void admm_colP(double* out) const {
+    for (int k = 0; k < P.N; ++k) {
+      for (int j = 0; j < 6; ++j) {
+        double mx = out[18 * k + j];
+        for (int i = 0; i < 6; ++i) mx = std::max(mx, std::fabs(aPq[36 * k + 6 * i + j]));
+        out[18 * k + j] = mx;
+      }
+      const int hi = k < P.N - 1 ? 18 : 12;
+      for (int i = 6; i < hi; ++i) out[18 * k + i] = std::max(out[18 * k + i], std::fabs(aPd[18 * k + i]));
+    }
+  }
+  // the new QP's linear cost, scaled (update(q)): q = c D g, g of src/osqp_solver.py:125-134
+  void admm_q(const R* X) {
+    for (int k = 0; k < P.N; ++k) {
+      const R* w = &cost[10 * k];
+      for (int i = 0; i < 6; ++i) aqs[18 * k + i] = val(w[6] * w[i]);
+      for (int i = 6; i < 12; ++i) aqs[18 * k + i] = val(w[7] * X[18 * k + i]);
+      if (k < P.N - 1)
+        for (int i = 12; i < 18; ++i) aqs[18 * k + i] = val(w[8] * X[18 * k + i]);
+    }
+  }
+
+  // block Cholesky of M = P_s + sigma I + A_s' rho A_s; every row is an equality row here
+  // (rho_vec = 1e3 rho, OSQP's RHO_EQ_OVER_RHO_INEQ)
+  void admm_factor(double rho) {
+    const int N = P.N;
+    const double re = 1e3 * rho;
+    double Cp[12][18];
+    for (int k = 0; k < N; ++k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      double S[18][18];
+      for (int a = 0; a < 18; ++a)
+        for (int b = 0; b < 18; ++b) S[a][b] = 0.0;
+      for (int a = 0; a < 6; ++a)
+        for (int b = 0; b < 6; ++b) S[a][b] = aPq[36 * k + 6 * a + b];
+      for (int a = 6; a < nk; ++a) S[a][a] = aPd[18 * k + a];
+      for (int a = 0; a < nk; ++a) S[a][a] += A_.sigma;
+      for (int a = 0; a < 12; ++a) S[a][a] += re * (aI[12 * k + a] * aI[12 * k + a]);
+      if (k < N - 1) {
+        const double* G = &aJ[216 * k];
+        for (int a = 0; a < 18; ++a)
+          for (int b = 0; b < 18; ++b) {
+            double acc = 0.0;
+            for (int i = 0; i < 12; ++i) acc += G[18 * i + a] * G[18 * i + b];
+            S[a][b] += re * acc;
+          }
+      }
+      if (k > 0)
+        for (int a = 0; a < 12; ++a)
+          for (int b = 0; b < 12; ++b) {
+            double acc = 0.0;
+            for (int j = 0; j < 18; ++j) acc += Cp[a][j] * Cp[b][j];
+            S[a][b] -= acc;
+          }
+      // right-looking Cholesky (the GPU's lane-parallel order)
+      for (int p = 0; p < nk; ++p) {
+        const double d = std::sqrt(S[p][p]);
+        S[p][p] = d;
+        const double id = 1.0 / d;
+        for (int i = p + 1; i < nk; ++i) S[i][p] = S[i][p] * id;
+        for (int i = p + 1; i < nk; ++i)
+          for (int j = p + 1; j <= i; ++j) S[i][j] = S[i][j] - S[i][p] * S[j][p];
+      }
+      double* Li = &aLinv[324 * k];
+      for (int i = 0; i < 324; ++i) Li[i] = 0.0;
+      for (int j = 0; j < nk; ++j) {
+        Li[18 * j + j] = 1.0 / S[j][j];
+        for (int i = j + 1; i < nk; ++i) {
+          double acc = 0.0;
+          for (int l = j; l < i; ++l) acc += S[i][l] * Li[18 * l + j];
+          Li[18 * i + j] = -acc / S[i][i];
+        }
+      }
+      if (k < N - 1) {
+        // C_k = M_{x_{k+1}, z_k} Linv_k', M_{x_{k+1}, z_k} = re diag(aI_{k+1}) G_k
+        const double* G = &aJ[216 * k];
+        double* C = &aC[216 * k];
+        for (int a = 0; a < 12; ++a)
+          for (int j = 0; j < 18; ++j) {
+            double acc = 0.0;
+            for (int l = 0; l <= j; ++l) acc += G[18 * a + l] * Li[18 * j + l];
+            C[18 * a + j] = Cp[a][j] = re * aI[12 * (k + 1) + a] * acc;
+          }
+      }
+    }
+  }
+  void admm_solve(const double* b, double* x) const {
+    const int N = P.N;
+    double w[64][18];
+    for (int k = 0; k < N; ++k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      double r[18];
+      for (int i = 0; i < nk; ++i) r[i] = b[18 * k + i];
+      if (k > 0) {
+        const double* C = &aC[216 * (k - 1)];
+        for (int a = 0; a < 12; ++a) {
+          double acc = 0.0;
+          for (int j = 0; j < 18; ++j) acc += C[18 * a + j] * w[k - 1][j];
+          r[a] -= acc;
+        }
+      }
+      const double* Li = &aLinv[324 * k];
+      for (int i = 0; i < nk; ++i) {
+        double acc = 0.0;
+        for (int j = 0; j <= i; ++j) acc += Li[18 * i + j] * r[j];
+        w[k][i] = acc;
+      }
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      double r[18];
+      for (int i = 0; i < nk; ++i) r[i] = w[k][i];
+      if (k < N - 1) {
+        const double* C = &aC[216 * k];
+        for (int j = 0; j < 18; ++j) {
+          double acc = 0.0;
+          for (int a = 0; a < 12; ++a) acc += C[18 * a + j] * x[18 * (k + 1) + a];
+          r[j] -= acc;
+        }
+      }
+      const double* Li = &aLinv[324 * k];
+      for (int j = 0; j < nk; ++j) {
+        double acc = 0.0;
+        for (int i = j; i < nk; ++i) acc += Li[18 * i + j] * r[i];
+        x[18 * k + j] = acc;
+      }
+    }
+  }
+  void admm_Ax(const double* x, double* o) const {
+    for (int i = 0; i < 12; ++i) o[i] = aI[i] * x[i];
+    for (int k = 0; k + 1 < P.N; ++k) {
+      const double* G = &aJ[216 * k];
+      for (int i = 0; i < 12; ++i) {
+        double acc = 0.0;
+        for (int j = 0; j < 18; ++j) acc += G[18 * i + j] * x[18 * k + j];
+        o[12 * (k + 1) + i] = acc + aI[12 * (k + 1) + i] * x[18 * (k + 1) + i];
+      }
+    }
+  }
+  void admm_Aty(const double* t, double* o) const {
+    for (int k = 0; k < P.N; ++k) {
+      const int nk = k < P.N - 1 ? 18 : 12;
+      for (int j = 0; j < nk; ++j) {
+        double acc = j < 12 ? aI[12 * k + j] * t[12 * k + j] : 0.0;
+        if (k < P.N - 1) {
+          const double* G = &aJ[216 * k];
+          for (int i = 0; i < 12; ++i) acc += G[18 * i + j] * t[12 * (k + 1) + i];
+        }
+        o[18 * k + j] = acc;
+      }
+    }
+  }
+  void admm_Px(const double* x, double* o) const {
+    for (int k = 0; k < P.N; ++k) {
+      const int nk = k < P.N - 1 ? 18 : 12;
+      for (int i = 0; i < 6; ++i) {
+        double acc = 0.0;
+        for (int j = 0; j < 6; ++j) acc += aPq[36 * k + 6 * i + j] * x[18 * k + j];
+        o[18 * k + i] = acc;
+      }
+      for (int i = 6; i < nk; ++i) o[18 * k + i] = aPd[18 * k + i] * x[18 * k + i];
+    }
+  }
+
+  // one QP: setup (scaling with the previous q), the new q, factor, OSQP's iteration from the
+  // state's warm start; sol = D x
+  void admm(const R* X, const R* xs, AdmmState& st) {
+    const int N = P.N, m = 12 * N;
+    admm_setup(X, xs, st.qold);
+    admm_q(X);
+    for (int e = 0; e < T; ++e) { st.qold[e] = aqs[e]; aqs[e] = ac * (aD[e] * aqs[e]); }
+    double rho = *st.rho;
+    admm_factor(rho);
+    double rv = 1e3 * rho, ri = 1.0 / rv;
+    std::vector<double> xt(T), zt(m), rhs(T), t(m), Ax(m), Px(T), Aty(T), xp(T);
+    double* x = st.x;
+    double* z = st.z;
+    double* y = st.y;
+    const double al = A_.alpha, sg = A_.sigma;
+    int it = 0;
+    bool checked = false;
+    admm_solved = 0;
+    for (it = 1; it <= A_.max_iter; ++it) {
+      for (int r = 0; r < m; ++r) t[r] = z[r] - ri * y[r];
+      for (int r = 0; r < m; ++r) t[r] = rv * t[r];
+      admm_Aty(t.data(), rhs.data());
+      for (int e = 0; e < T; ++e) rhs[e] = (sg * x[e] - aqs[e]) + rhs[e];
+      admm_solve(rhs.data(), xt.data());
+      admm_Ax(xt.data(), zt.data());
+      for (int e = 0; e < T; ++e) x[e] = al * xt[e] + (1.0 - al) * x[e];
+      for (int r = 0; r < m; ++r) {
+        const double zr = al * zt[r] + (1.0 - al) * z[r];
+        double zn = zr + ri * y[r];
+        zn = std::min(std::max(zn, als[r]), als[r]);
+        y[r] = y[r] + rv * (zr - zn);
+        z[r] = zn;
+      }
+      checked = A_.check && it % A_.check == 0;
+      bool adapt = A_.adapt_interval && it % A_.adapt_interval == 0;
+      if (checked || adapt) {
+        admm_Ax(x, Ax.data());
+        admm_Px(x, Px.data());
+        admm_Aty(y, Aty.data());
+      }
+      if (checked && admm_converged(x, z, y, Ax.data(), Px.data(), Aty.data())) {
+        admm_solved = 1;
+        break;
+      }
+      if (adapt) {
+        double pri = 0.0, pn = 0.0, dua = 0.0, dn = 0.0;
+        for (int r = 0; r < m; ++r) {
+          pri = std::max(pri, std::fabs(Ax[r] - z[r]));
+          pn = std::max(pn, std::max(std::fabs(z[r]), std::fabs(Ax[r])));
+        }
+        for (int e = 0; e < T; ++e) {
+          dua = std::max(dua, std::fabs(aqs[e] + Px[e] + Aty[e]));
+          dn = std::max(dn, std::max(std::fabs(aqs[e]), std::max(std::fabs(Aty[e]), std::fabs(Px[e]))));
+        }
+        pri = pri / (pn + 1e-30);
+        dua = dua / (dn + 1e-30);
+        double rn = rho * std::sqrt(pri / (dua + 1e-30));
+        rn = std::min(std::max(rn, 1e-6), 1e6);
+        if (rn > rho * A_.adapt_tol || rn < rho / A_.adapt_tol) {
+          rho = rn;
+          rv = 1e3 * rho;
+          ri = 1.0 / rv;
+          admm_factor(rho);
+        }
+      }
+    }
+    admm_it = it > A_.max_iter ? A_.max_iter : it;
+    *st.rho = rho;
+    for (int e = 0; e < T; ++e) sol[e] = R(aD[e] * x[e]);
+  }
+  // OSQP's check_termination on the unscaled residuals, with OSQP 1.x's duality-gap test
+  bool admm_converged(const double* x, const double* z, const double* y, const double* Ax, const double* Px,
+                      const double* Aty) const {
+    const int m = 12 * P.N;
+    const double cinv = 1.0 / ac;
+    double pr = 0.0, zn = 0.0, an = 0.0;
+    for (int r = 0; r < m; ++r) {
+      const double ei = 1.0 / aE[r];
+      pr = std::max(pr, std::fabs(ei * (Ax[r] - z[r])));
+      zn = std::max(zn, std::fabs(ei * z[r]));
+      an = std::max(an, std::fabs(ei * Ax[r]));
+    }
+    double dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0, xPx = 0.0, qx = 0.0;
+    for (int e = 0; e < T; ++e) {
+      const double di = 1.0 / aD[e];
+      dr = std::max(dr, std::fabs(di * ((aqs[e] + Px[e]) + Aty[e])));
+      qn = std::max(qn, std::fabs(di * aqs[e]));
+      atn = std::max(atn, std::fabs(di * Aty[e]));
+      pxn = std::max(pxn, std::fabs(di * Px[e]));
+      xPx += x[e] * Px[e];
+      qx += aqs[e] * x[e];
+    }
+    dr *= cinv;
+    if (!(pr < A_.eps_abs + A_.eps_rel * std::max(zn, an))) return false;
+    if (!(dr < A_.eps_abs + A_.eps_rel * cinv * std::max(qn, std::max(atn, pxn)))) return false;
+    if (A_.gap) {
+      double sc = 0.0;
+      for (int r = 0; r < m; ++r) sc += als[r] * std::max(y[r], 0.0) + als[r] * std::min(y[r], 0.0);
+      xPx *= cinv; qx *= cinv; sc *= cinv;
+      const double gap = xPx + qx + sc;
+      if (!(std::fabs(gap) < A_.eps_abs + A_.eps_rel * std::max(std::fabs(xPx), std::max(std::fabs(qx), std::fabs(sc)))))
+        return false;
+    }
+    return true;
+  }
+
   // returns qp_iters; alphas/steps filled
   // box mode: ipm_it[qp] = the interior point's iterations of SQP iteration qp (may be null)
+  // ADMM mode (st non-null): admm_it[qp] = OSQP iterations of SQP iteration qp
   int sqp(R* X, const R* xs, const double* goal, const double* f6, double* alphas, double* steps, int* n_alpha,
-          int* n_step, int* ipm_it = nullptr) {
+          int* n_step, int* ipm_it = nullptr, AdmmState* st = nullptr, int* admm_its = nullptr) {
     static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
     std::vector<R> Xn(T);
     *n_alpha = *n_step = 0;
     int qp = 0;
     for (qp = 0; qp < P.max_iters; ++qp) {
       linearize(X, goal, f6);
-      riccati(X, xs);
+      if (st) {
+        admm(X, xs, *st);
+        if (admm_its) admm_its[qp] = admm_it;
+      } else {
+        riccati(X, xs);
+      }
       if (P.box_mask) {
         ipm(X, xs);
         if (ipm_it) ipm_it[qp] = ipm_iters;
@@ -974,6 +1382,42 @@ int i7m_cpu_solve_box(const double* model_packed, int N, const double* cfg, cons
                         ipm_iters ? ipm_iters + 8 * (size_t)b : nullptr);
     if (ipm_conv) ipm_conv[b] = S.ipm_conv;
     if (ipm_mu) ipm_mu[b] = S.ipm_mu;
+  }
+  return 0;
+}
+
+// ADMM mode (OSQP's algorithm, oracle/osqp_admm.py): admm_cfg = rho0, sigma, alpha, eps_abs,
+// eps_rel, max_iter, check_termination, scaling, check_dualgap, adaptive_rho_interval,
+// adaptive_rho_tolerance.  The solver state of every problem (scaled x (B, T), z (B, 12N),
+// y (B, 12N), the previous QP's q (B, T), rho (B)) is read and written back: it is the
+// reference's OSQP object, warm-started from call to call (src/osqp_solver.py:38-40).
+// admm_iters (B, 8): OSQP iterations per SQP iteration (may be null).
+int i7m_cpu_solve_admm(const double* model_packed, int N, const double* cfg, const double* admm_cfg, int B,
+                       const double* xu_in, const double* xcur, const double* goals, int goal_stride,
+                       const double* fext, double* xu_out, int* qp_iters, double* alphas, double* steps,
+                       double* st_x, double* st_z, double* st_y, double* st_q, double* st_rho, int* admm_iters,
+                       int nthreads) {
+  if (N < 2 || N > 64 || B < 0 || !admm_cfg) return -1;
+  const Model M = make_model(model_packed);
+  Params P = make_params(N, cfg, goal_stride);
+  AdmmParams A;
+  A.rho0 = admm_cfg[0]; A.sigma = admm_cfg[1]; A.alpha = admm_cfg[2]; A.eps_abs = admm_cfg[3]; A.eps_rel = admm_cfg[4];
+  A.max_iter = (int)admm_cfg[5]; A.check = (int)admm_cfg[6]; A.scaling = (int)admm_cfg[7]; A.gap = (int)admm_cfg[8];
+  A.adapt_interval = (int)admm_cfg[9]; A.adapt_tol = admm_cfg[10];
+  const int T = 18 * N - 6, m = 12 * N;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int b = 0; b < B; ++b) {
+    Solver<double> S(M, P);
+    S.A_ = A;
+    S.admm_alloc();
+    Solver<double>::AdmmState st{st_x + (size_t)b * T, st_z + (size_t)b * m, st_y + (size_t)b * m, st_q + (size_t)b * T,
+                                 st_rho + b};
+    double* X = xu_out + (size_t)b * T;
+    std::memcpy(X, xu_in + (size_t)b * T, sizeof(double) * T);
+    int na, ns;
+    qp_iters[b] = S.sqp(X, xcur + 12 * (size_t)b, goals + (size_t)b * N * goal_stride, fext ? fext + 6 * (size_t)b : nullptr,
+                        alphas + 8 * (size_t)b, steps + 8 * (size_t)b, &na, &ns, nullptr, &st,
+                        admm_iters ? admm_iters + 8 * (size_t)b : nullptr);
   }
   return 0;
 }

@@ -28,6 +28,8 @@ def load(path=None):
         _lib.i7m_cpu_solve_box.argtypes = [_DP, C.c_int, _DP, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP,
                                            _DP, _DP, _IP, _IP, _DP, C.c_int]
         _lib.i7m_cpu_count_flops_box.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, _DP, C.c_int, _DP]
+        _lib.i7m_cpu_solve_admm.argtypes = [_DP, C.c_int, _DP, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP,
+                                            _DP, _DP, _DP, _DP, _DP, _DP, _DP, _IP, C.c_int]
     return _lib
 
 
@@ -91,6 +93,56 @@ def solve_box(xcur, goals, XU, N, nthreads=1, fext=None, box=None, **cfg):
     if rc != 0:
         raise RuntimeError("i7m_cpu_solve_box failed")
     return out, qp, al, st, it, conv, mu
+
+
+def admm_cfg(rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, max_iter=4000, check_termination=25,
+             scaling=10, check_dualgap=True, adaptive_rho_interval=0, adaptive_rho_tolerance=5.0):
+    """ADMM mode settings: OSQP's defaults as oracle/osqp_admm.py pins them (gap test on, no rho
+    adaptation)."""
+    return np.array([rho, sigma, alpha, eps_abs, eps_rel, max_iter, check_termination, scaling, float(check_dualgap),
+                     adaptive_rho_interval, adaptive_rho_tolerance], dtype=np.float64)
+
+
+class AdmmState:
+    """Per-problem OSQP solver state (scaled x, z, y, the previous QP's q, rho), carried from
+    call to call as the reference's OSQP object carries it."""
+
+    def __init__(self, B, N, rho=0.1):
+        T, m = 18 * N - 6, 12 * N
+        self.x = np.zeros((B, T))
+        self.z = np.zeros((B, m))
+        self.y = np.zeros((B, m))
+        self.q = np.zeros((B, T))
+        self.rho = np.full(B, float(rho))
+
+
+def solve_admm(xcur, goals, XU, N, state, nthreads=1, fext=None, admm=None, **cfg):
+    """ADMM mode: (XU out, qp_iters, alphas, steps, OSQP iterations (B, 8) per SQP iteration);
+    `state` (AdmmState) is updated in place."""
+    lib = load()
+    XU = np.ascontiguousarray(XU, float)
+    B = XU.shape[0]
+    xcur = np.ascontiguousarray(xcur, float)
+    goals = np.ascontiguousarray(goals, float)
+    stride = goals.shape[1] // N
+    out = np.empty_like(XU)
+    qp = np.zeros(B, dtype=np.int32)
+    al = np.full((B, 8), np.nan)
+    st = np.full((B, 8), np.nan)
+    it = np.full((B, 8), -1, dtype=np.int32)
+    f = np.ascontiguousarray(fext, float) if fext is not None else None
+    m = model_packed()
+    c = _cfg(**cfg)
+    ac = admm_cfg() if admm is None else np.asarray(admm, float)
+    for a in (state.x, state.z, state.y, state.q, state.rho):
+        assert a.flags.c_contiguous and a.dtype == np.float64 and a.shape[0] == B
+    rc = lib.i7m_cpu_solve_admm(_p(m), N, _p(c), _p(ac), B, _p(XU), _p(xcur), _p(goals), stride,
+                                _p(f) if f is not None else None, _p(out), qp.ctypes.data_as(_IP), _p(al), _p(st),
+                                _p(state.x), _p(state.z), _p(state.y), _p(state.q), _p(state.rho),
+                                it.ctypes.data_as(_IP), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("i7m_cpu_solve_admm failed")
+    return out, qp, al, st, it
 
 
 def solve(xcur, goals, XU, N, nthreads=1, fext=None, **cfg):

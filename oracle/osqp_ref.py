@@ -44,7 +44,8 @@ class OSQPSolverRef:
     """Restates OSQPSolver (src/osqp_solver.py:6-155); QP solved exactly."""
 
     def __init__(self, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
-                 qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30, fext6=None, fext_frame="local"):
+                 qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30, fext6=None, fext_frame="local",
+                 osqp_settings=None):
         self.P_ = P or rbd.params()
         # external wrench on joint 6 in every dynamics evaluation (batch_sqp's
         # set_external_wrench_batch; frame "world": converted per configuration, rbd.fext_list)
@@ -73,6 +74,11 @@ class OSQPSolverRef:
                               np.vstack([np.hstack([np.eye(nq), self.dt * np.eye(nq)]), np.ones((nq, 2 * nq))])])
         self.B_k = np.zeros((self.nx, self.nq))
         self.cx_k = np.zeros(self.nx)
+        if qp == "osqp":
+            # src/osqp_solver.py:38-40: one OSQP workspace, set up on the templates
+            from .osqp_admm import OSQP
+            self.osqp = OSQP()
+            self.osqp.setup(P=self.P, q=self.g, A=self.A, l=self.l, u=self.l, **(osqp_settings or {}))
 
     # src/osqp_solver.py:48-52
     def initialize_P(self):
@@ -203,6 +209,13 @@ class OSQPSolverRef:
     def setup_and_solve_qp(self, xu, xs, eepos_g):
         self.update_constraint_matrix(xu, xs)
         self.update_cost_matrix(xu, eepos_g)
+        if self.qp == "osqp":
+            # src/osqp_solver.py:140-143
+            self.osqp.update(Px=self.Pdata)
+            self.osqp.update(Ax=self.Adata)
+            self.osqp.update(q=self.g, l=self.l, u=self.l)
+            x, y = self.osqp.solve()
+            return QPResult(x, y, self.osqp.info["iter"])
         if self.qp == "admm":
             return self.solve_qp_admm()
         if self.qp == "box":
