@@ -18,7 +18,11 @@
  *                              (returns the QP minimiser sol.x, solved exactly; with
  *                               qp_mode = I7M_QP_BOX the QP also carries box rows on q, v, u
  *                               — SURVEY.md §8d config 4, an extension without a reference
- *                               counterpart; see oracle/box_ipm.py for its definition)
+ *                               counterpart; see oracle/box_ipm.py for its definition; with
+ *                               qp_mode = I7M_QP_ADMM it is OSQP's iterate, as the reference's
+ *                               osqp.solve() returns it, src/osqp_solver.py:38-40,140-143)
+ *   i7m_admm_reset             a fresh OSQP object / batch_sqp resetRho, resetLambda
+ *                                                             gato_controller.py:132-138
  *   i7m_linearize              update_constraint_matrix + update_cost_matrix
  *                                                             src/osqp_solver.py:70-135
  *   i7m_merit                  SQP_OSQP.eepos_cost + integrator_err
@@ -38,16 +42,18 @@
  *   goals (B, N*goal_stride), goal_stride 3 (OSQP surface, src/osqp_solver.py:111) or
  *         6 (batch_sqp surface, gato_controller.py:180-183; first 3 of each 6 used)
  *
- * Deviations from the C-ABI sketched in SURVEY.md §8(b):
- *   - no ADMM mode (`qp_mode` admm): I7M_QP_DIRECT solves each SQP subproblem QP exactly (the
- *     optimum OSQP's ADMM approximates to eps 1e-3, src/osqp_solver.py:39-41); box rows
- *     (config 4) use an interior point whose Newton steps are the same exact solve — measured
- *     against ADMM in DESIGN.md §4.4 (ADMM needed 40-4700 iterations on those problems);
- *   - no `precision` field: every kernel computes in fp64.  The drop-in batch_sqp module keeps
- *     the reference's SQPSolverfloat_* class names (gato_controller.py:54-62) so callers run
- *     unchanged, but it also solves (and returns) fp64;
- *   - i7m_reset exists but has little to reset: the exact solve keeps no warm start, penalty
- *     or dual state between calls (the reference's OSQP warm start, src/osqp_solver.py:140-143).
+ * QP modes (SURVEY.md §8(b) `qp_mode {direct, admm}`):
+ *   - I7M_QP_DIRECT solves each SQP subproblem QP exactly (the optimum OSQP's ADMM approximates to
+ *     eps 1e-3, src/osqp_solver.py:39-41) and keeps no state between calls;
+ *   - I7M_QP_ADMM runs OSQP's algorithm itself (oracle/osqp_admm.py, pinned by the reference's
+ *     printed closed loop): per problem a solver state (iterates, rho, the previous QP's linear
+ *     cost) carried from call to call like the reference's osqp.OSQP object — i7m_reset or
+ *     i7m_admm_reset start it afresh;
+ *   - I7M_QP_BOX (config 4) adds box rows, solved by an interior point whose Newton steps are the
+ *     exact solve (ADMM needed 40-4700 iterations on those problems).
+ * Deviation: no `precision` field: every kernel computes in fp64.  The drop-in batch_sqp module
+ * keeps the reference's SQPSolverfloat_* class names (gato_controller.py:54-62) so callers run
+ * unchanged, but it also solves (and returns) fp64.
  *
  * Status: 0 = OK, <0 = error (see I7M_E*), message via i7m_last_error() (thread-local).
  * Threading: a handle is not re-entrant (like the reference's stateful OSQPSolver);
@@ -69,13 +75,15 @@ extern "C" {
 #define I7M_MAX_N 64
 
 /* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
- * layout, field meaning or enum count changes.  3: i7m_config's former `pad` is `h2h_chunks` (a
+ * layout, field meaning or enum count changes.  4: I7M_QP_ADMM and i7m_config's admm_* fields
+ * (appended), I7M_K_COUNT 9 (I7M_K_ADMM), i7m_admm_reset / i7m_get_admm_stats /
+ * i7m_get_admm_state (0.4 builds).  3: i7m_config's former `pad` is `h2h_chunks` (a
  * nonzero value changes how i7m_solve runs; outside [0, 64] it is refused) and I7M_K_COUNT is 8
  * (I7M_K_LINESEARCH_TAIL added) — size timing arrays from I7M_K_COUNT of this header (0.3 builds).
  * 2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and i7m_set_external_wrench a
  * trailing `frame` (0.2 builds); 1 had neither.  A caller built against another revision must not
  * call through this library: compare first. */
-#define I7M_ABI_VERSION 3
+#define I7M_ABI_VERSION 4
 
 #define I7M_OK 0
 #define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */
@@ -83,7 +91,7 @@ extern "C" {
 #define I7M_ENOMEM -3   /* device allocation failed */
 #define I7M_ENODEV -4   /* no usable gfx950 device */
 
-enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1 };
+enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1, I7M_QP_ADMM = 2 };
 /* How a solve is launched (I7M_QP_DIRECT): FUSED = one kernel per solve (a workgroup per
  * problem runs every SQP iteration's linearisation, QP and line search), FUSED_ITER = that kernel
  * once per SQP iteration, SPLIT = three kernels per SQP iteration; AUTO = SPLIT at every batch
@@ -119,7 +127,8 @@ typedef struct i7m_config {
   int32_t max_batch;    /* device buffers are sized for this many problems */
   int32_t device_id;
   int32_t qp_mode;      /* I7M_QP_DIRECT: exact block-tridiagonal (Riccati) KKT solve;
-                           I7M_QP_BOX: + box rows on q, v, u (interior point, Riccati Newton steps) */
+                           I7M_QP_BOX: + box rows on q, v, u (interior point, Riccati Newton steps);
+                           I7M_QP_ADMM: OSQP's ADMM with its warm-started state */
   i7m_model model;
   /* I7M_QP_BOX only (appended: the offsets above are unchanged) */
   int32_t box_mask;     /* which rows: I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U (default all) */
@@ -129,6 +138,21 @@ typedef struct i7m_config {
   int32_t h2h_chunks;   /* i7m_solve (host buffers): split the batch into this many chunks, copies in,
                            solves and copies out pipelined on three streams so copies overlap
                            solves; 0 = automatic (was `pad`: same layout) */
+  /* I7M_QP_ADMM only (appended): OSQP's settings; defaults (i7m_config_default) are OSQP's own
+     with the duality-gap test on and no rho adaptation — the combination that reproduces the
+     reference's printed closed loop (oracle/osqp_admm.py) */
+  double admm_rho;              /* 0.1; equality rows use 1e3 rho (all of this QP's rows) */
+  double admm_sigma;            /* 1e-6 */
+  double admm_alpha;            /* relaxation, 1.6 */
+  double admm_eps_abs;          /* 1e-3 */
+  double admm_eps_rel;          /* 1e-3 */
+  int32_t admm_max_iter;        /* 4000 */
+  int32_t admm_check_termination; /* 25: residuals are tested every this many iterations */
+  int32_t admm_scaling;         /* Ruiz passes, 10 */
+  int32_t admm_check_dualgap;   /* 1: OSQP 1.x's duality-gap test */
+  int32_t admm_adaptive_rho_interval; /* 0: never adapt rho; else every this many iterations */
+  int32_t admm_pad;
+  double admm_adaptive_rho_tolerance; /* 5 */
 } i7m_config;
 
 /* Per-problem SQP statistics (keys of SQP_OSQP.stats, src/osqp_sqp.py:7-11). */
@@ -155,9 +179,10 @@ void i7m_destroy(i7m_handle* h);
 int i7m_set_stream(i7m_handle* h, void* stream);
 /* Back to the post-create solver state (batch_sqp reset / resetRho / resetLambda,
  * gato_controller.py:132-138): waits for the handle's stream, drops captured solve graphs and
- * zeroes the kernel timing sums.  The exact solve carries no warm start, penalty or dual state
- * across calls, so results never depend on earlier calls either way.  The external wrench is
- * caller input like the model and is kept: clear it with i7m_set_external_wrench(h, 0, NULL, 0). */
+ * zeroes the kernel timing sums; I7M_QP_ADMM: every problem's OSQP state starts afresh
+ * (i7m_admm_reset(h, max_batch, I7M_ADMM_RESET_ALL)).  The exact modes carry no warm start,
+ * penalty or dual state across calls.  The external wrench is caller input like the model and is
+ * kept: clear it with i7m_set_external_wrench(h, 0, NULL, 0). */
 int i7m_reset(i7m_handle* h);
 int i7m_synchronize(i7m_handle* h);
 
@@ -210,6 +235,21 @@ int i7m_qp_value(i7m_handle* h, int32_t B, const double* xu, const double* xcur,
  * (mu < box_tol and residuals reduced by box_tol), final mu.  Any output may be NULL. */
 int i7m_get_box_stats(i7m_handle* h, int32_t B, int32_t* iters, int32_t* converged, double* mu);
 
+/* I7M_QP_ADMM: start the OSQP state of problems [0, B) afresh.  what: I7M_ADMM_RESET_RHO (rho back
+ * to admm_rho; batch_sqp resetRho), _DUAL (y = 0; resetLambda), _PRIMAL (x = z = 0 and the
+ * remembered linear cost = 0), _ALL (a new OSQP object: the state right after create). */
+#define I7M_ADMM_RESET_RHO 1
+#define I7M_ADMM_RESET_DUAL 2
+#define I7M_ADMM_RESET_PRIMAL 4
+#define I7M_ADMM_RESET_ALL 7
+int i7m_admm_reset(i7m_handle* h, int32_t B, int32_t what);
+/* I7M_QP_ADMM: OSQP iterations of every SQP iteration of the last solve (B, I7M_MAX_SQP; -1 where
+ * the problem ran no QP) and the current rho (B).  Either may be NULL. */
+int i7m_get_admm_stats(i7m_handle* h, int32_t B, int32_t* iters, double* rho);
+/* I7M_QP_ADMM: the carried OSQP state of problems [0, B) in OSQP's scaled coordinates: x (B, T),
+ * z, y (B, 12N), the previous QP's linear cost, unscaled (B, T), rho (B).  Any may be NULL. */
+int i7m_get_admm_state(i7m_handle* h, int32_t B, double* x, double* z, double* y, double* q, double* rho);
+
 /* Raw linearisation at xu.  lin (B, N-1, 114): per knot Aq(6x6,row-major, =dt*da/dq),
  * Av (=I+dt*da/dv), Bu (=dt*Minv), a (=ABA(q,v,u)); cost (B, N, 10): j = J^T e (6),
  * Qm, dQm, Rm, |e|.  Either output may be NULL. */
@@ -250,7 +290,8 @@ int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* en
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,
-       I7M_K_SQP_FUSED = 6, I7M_K_LINESEARCH_TAIL = 7 /* second launch of a split line search */, I7M_K_COUNT = 8 };
+       I7M_K_SQP_FUSED = 6, I7M_K_LINESEARCH_TAIL = 7 /* second launch of a split line search */, I7M_K_ADMM = 8,
+       I7M_K_COUNT = 9 };
 int i7m_set_timing(i7m_handle* h, int enable);
 /* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
 int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);

@@ -20,17 +20,17 @@ import numpy as np
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
-ABI_VERSION = 3  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
+ABI_VERSION = 4  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8
 MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
 (I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_SQP_FUSED,
- I7M_K_LINESEARCH_TAIL) = range(8)
-I7M_K_COUNT = 8
+ I7M_K_LINESEARCH_TAIL, I7M_K_ADMM) = range(9)
+I7M_K_COUNT = 9
 KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused", "k_sqp_fused",
-                "k_linesearch_tail")
+                "k_linesearch_tail", "k_admm")
 
 
 class I7MError(RuntimeError):
@@ -73,10 +73,26 @@ class i7m_config(C.Structure):
         ("box_tol", C.c_double),
         ("pipeline", C.c_int32),
         ("h2h_chunks", C.c_int32),
+        ("admm_rho", C.c_double),
+        ("admm_sigma", C.c_double),
+        ("admm_alpha", C.c_double),
+        ("admm_eps_abs", C.c_double),
+        ("admm_eps_rel", C.c_double),
+        ("admm_max_iter", C.c_int32),
+        ("admm_check_termination", C.c_int32),
+        ("admm_scaling", C.c_int32),
+        ("admm_check_dualgap", C.c_int32),
+        ("admm_adaptive_rho_interval", C.c_int32),
+        ("admm_pad", C.c_int32),
+        ("admm_adaptive_rho_tolerance", C.c_double),
     ]
 
 
-QP_DIRECT, QP_BOX = 0, 1
+QP_DIRECT, QP_BOX, QP_ADMM = 0, 1, 2
+ADMM_RESET_RHO, ADMM_RESET_DUAL, ADMM_RESET_PRIMAL, ADMM_RESET_ALL = 1, 2, 4, 7
+# OSQP's settings as i7m_config_default sets them (oracle/osqp_admm.py DEFAULTS)
+ADMM_DEFAULTS = dict(rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, max_iter=4000, check_termination=25,
+                     scaling=10, check_dualgap=True, adaptive_rho_interval=0, adaptive_rho_tolerance=5.0)
 PIPE_AUTO, PIPE_SPLIT, PIPE_FUSED, PIPE_FUSED_ITER = 0, 1, 2, 3
 WRENCH_LOCAL, WRENCH_WORLD = 0, 1
 _FRAMES = {"local": WRENCH_LOCAL, "world": WRENCH_WORLD, WRENCH_LOCAL: WRENCH_LOCAL, WRENCH_WORLD: WRENCH_WORLD}
@@ -121,6 +137,9 @@ SIGNATURES = [
     ("i7m_qp", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_qp_value", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_get_box_stats", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _DP]),
+    ("i7m_admm_reset", C.c_int, [_H, C.c_int32, C.c_int32]),
+    ("i7m_get_admm_stats", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32), _DP]),
+    ("i7m_get_admm_state", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, _DP]),
     ("i7m_linearize", C.c_int, [_H, C.c_int32, _DP, _DP, C.c_int32, _DP, _DP]),
     ("i7m_merit", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_linesearch", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
@@ -197,7 +216,10 @@ class Handle:
 
     def __init__(self, model, N=32, dt=0.01, dQ_cost=0.01, R_cost=1e-5, QN_cost=100.0, regularize=True, eps=1.0,
                  max_batch=1, device_id=0, mu=10.0, step_tol=1e-3, max_sqp_iters=2, qp_mode=QP_DIRECT,
-                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8, pipeline=PIPE_AUTO, h2h_chunks=0):
+                 box_mask=BOX_Q | BOX_V | BOX_U, box_max_iters=30, box_tol=1e-8, pipeline=PIPE_AUTO, h2h_chunks=0,
+                 admm=None):
+        """admm: OSQP settings for qp_mode=QP_ADMM (keys of ADMM_DEFAULTS; missing keys keep the
+        defaults)."""
         lib = load()
         cfg = i7m_config()
         _check(lib.i7m_config_default(C.byref(cfg)))
@@ -207,6 +229,13 @@ class Handle:
         cfg.qp_mode, cfg.box_mask, cfg.box_max_iters, cfg.box_tol = int(qp_mode), int(box_mask), int(box_max_iters), float(box_tol)
         cfg.pipeline = int(pipeline)
         cfg.h2h_chunks = int(h2h_chunks)
+        if admm:
+            unknown = set(admm) - set(ADMM_DEFAULTS)
+            if unknown:
+                raise ValueError(f"unknown ADMM settings {sorted(unknown)}")
+            for k, v in admm.items():
+                f = "admm_" + k
+                setattr(cfg, f, type(getattr(cfg, f))(v) if not isinstance(v, bool) else int(v))
         packed = np.ascontiguousarray(model.packed(), dtype=np.float64)
         assert packed.nbytes == C.sizeof(i7m_model), (packed.nbytes, C.sizeof(i7m_model))
         C.memmove(C.byref(cfg.model), packed.ctypes.data, packed.nbytes)
@@ -295,6 +324,29 @@ class Handle:
         ip = C.POINTER(C.c_int32)
         _check(self._lib.i7m_get_box_stats(self._h, int(B), it.ctypes.data_as(ip), cv.ctypes.data_as(ip), _ptr(mu)))
         return it, cv.astype(bool), mu
+
+    def admm_reset(self, B=None, what=ADMM_RESET_ALL):
+        """I7M_QP_ADMM: start the OSQP state of problems [0, B) afresh (what: ADMM_RESET_* bits;
+        RHO = batch_sqp resetRho, DUAL = resetLambda, ALL = a new OSQP object)."""
+        _check(self._lib.i7m_admm_reset(self._h, int(self.max_batch if B is None else B), int(what)))
+
+    def admm_stats(self, B):
+        """I7M_QP_ADMM: (OSQP iterations per SQP iteration of the last solve (B, 8), -1 = none;
+        rho (B,))."""
+        it = np.zeros((B, MAX_SQP), dtype=np.int32)
+        rho = np.zeros(B)
+        _check(self._lib.i7m_get_admm_stats(self._h, int(B), it.ctypes.data_as(C.POINTER(C.c_int32)), _ptr(rho)))
+        return it, rho
+
+    def admm_state(self, B):
+        """I7M_QP_ADMM: the carried OSQP state (scaled x (B, T), z, y (B, 12N), previous q (B, T),
+        rho (B,))."""
+        m = 12 * self.N
+        x, q = np.empty((B, self.T)), np.empty((B, self.T))
+        z, y = np.empty((B, m)), np.empty((B, m))
+        rho = np.empty(B)
+        _check(self._lib.i7m_get_admm_state(self._h, int(B), _ptr(x), _ptr(z), _ptr(y), _ptr(q), _ptr(rho)))
+        return x, z, y, q, rho
 
     def linearize(self, xu, goals):
         xu, goals, B, stride = self._batch(xu, goals)
@@ -400,6 +452,6 @@ class Handle:
         _check(self._lib.i7m_reset_kernel_times(self._h))
 
     def reset(self):
-        """i7m_reset: back to the post-create solver state (no warm start exists to clear; drops
-        captured graphs and timing sums; the external wrench is kept)."""
+        """i7m_reset: back to the post-create solver state (ADMM mode: every problem's OSQP state
+        afresh; drops captured graphs and timing sums; the external wrench is kept)."""
         _check(self._lib.i7m_reset(self._h))

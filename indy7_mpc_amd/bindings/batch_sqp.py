@@ -4,8 +4,10 @@
 The reference binding is an external CUDA module (absent).  This one keeps its
 Python surface — ``SQPSolverfloat_{1..256}`` with ``solve``, ``reset``, ``resetRho``,
 ``resetLambda``, ``set_external_wrench_batch`` and ``sim_forward`` — and solves the OSQP
-formulation of src/osqp_solver.py (fp64, exact QP) on the GPU.  N is taken from the XU width
-(traj_len = 18N - 6); goals use the GATO layout (B, 6N), first 3 of every 6 used.
+formulation of src/osqp_solver.py (fp64) on the GPU, each QP exactly (default) or, with
+``qp_mode="admm"``, by OSQP's own iteration from a per-problem warm-started state (then
+``resetRho`` / ``resetLambda`` reset OSQP's rho / duals, gato_controller.py:132-138).  N is taken
+from the XU width (traj_len = 18N - 6); goals use the GATO layout (B, 6N), first 3 of every 6 used.
 
 External wrench convention (``set_external_wrench_batch``): by default each row is what the
 reference's callers put there — a WORLD-frame force [f; n] (gato_controller.py:77-81,120-129 and
@@ -31,9 +33,12 @@ _SIZES = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 class _SQPSolverBatch:
     batch_size = 1
 
-    def __init__(self, model=None, device_id=0, wrench_frame="world"):
+    def __init__(self, model=None, device_id=0, wrench_frame="world", qp_mode="direct"):
         if wrench_frame not in ("world", "local"):
             raise ValueError("wrench_frame must be 'world' or 'local'")
+        if qp_mode not in ("direct", "admm"):
+            raise ValueError("qp_mode must be 'direct' or 'admm'")
+        self.qp_mode = _lib.QP_ADMM if qp_mode == "admm" else _lib.QP_DIRECT
         self.model = model or default_model()
         self.device_id = device_id
         self.wrench_frame = wrench_frame
@@ -44,7 +49,8 @@ class _SQPSolverBatch:
 
     def _handle(self, N, dt):
         if self._key != (N, dt):
-            self._h = _lib.Handle(self.model, N=N, dt=dt, max_batch=self.batch_size, device_id=self.device_id)
+            self._h = _lib.Handle(self.model, N=N, dt=dt, max_batch=self.batch_size, device_id=self.device_id,
+                                  qp_mode=self.qp_mode)
             self._key = (N, dt)
             if np.any(self._fext):
                 self._h.set_external_wrench(self._fext, self.wrench_frame)
@@ -65,28 +71,42 @@ class _SQPSolverBatch:
         ls = []
         for it in range(iters):
             ls.append({"step_size": np.array([s["alphas"][it] if it < s["n_alphas"] else 0.0 for s in st])})
+        if self.qp_mode == _lib.QP_ADMM:  # inner iterations per SQP iteration: OSQP's
+            adm = h.admm_stats(self.batch_size)[0]
+            inner = [{"pcg_iterations": np.maximum(adm[:, it], 0)} for it in range(iters)]
+        else:
+            inner = [{"pcg_iterations": 0} for _ in range(iters)]  # exact KKT solve, no PCG
         return {
             "xu_trajectory": out,
             "solve_time_us": (t1 - t0) * 1e6,
             "sqp_iterations": st["qp_iters"].copy(),
-            "pcg_stats": [{"pcg_iterations": 0} for _ in range(iters)],  # exact KKT solve, no PCG
+            "pcg_stats": inner,
             "line_search_stats": ls,
         }
 
     def reset(self):
-        """Solver state reset (i7m_reset): the exact solve keeps no warm start between calls, so
-        results are unchanged; the wrench hypotheses are kept."""
+        """Solver state reset (i7m_reset): ADMM mode starts every problem's OSQP state afresh;
+        the exact solve keeps no warm start, so its results are unchanged; the wrench hypotheses
+        are kept."""
         for h in (self._h, self._sim):
             if h is not None:
                 h.reset()
 
     def resetRho(self):
-        """ADMM/PCG penalty reset: the exact solve has no penalty, so this is i7m_reset."""
-        self.reset()
+        """Penalty reset: ADMM mode puts OSQP's rho back to its setting (the iterates stay);
+        the exact solve has no penalty, so there it is i7m_reset."""
+        if self.qp_mode == _lib.QP_ADMM and self._h is not None:
+            self._h.admm_reset(what=_lib.ADMM_RESET_RHO)
+        else:
+            self.reset()
 
     def resetLambda(self):
-        """Dual reset: the exact solve keeps no duals between calls, so this is i7m_reset."""
-        self.reset()
+        """Dual reset: ADMM mode zeroes OSQP's y; the exact solve keeps no duals, so there it is
+        i7m_reset."""
+        if self.qp_mode == _lib.QP_ADMM and self._h is not None:
+            self._h.admm_reset(what=_lib.ADMM_RESET_DUAL)
+        else:
+            self.reset()
 
     def set_external_wrench_batch(self, f_ext_batch):
         f = np.asarray(f_ext_batch, dtype=float).reshape(self.batch_size, 6)

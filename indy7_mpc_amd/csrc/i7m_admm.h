@@ -1,0 +1,493 @@
+// i7m_admm.h — ADMM mode (I7M_QP_ADMM): the reference's QP solver, OSQP, as a device kernel.
+//
+// The reference solves every SQP subproblem with one persistent osqp.OSQP() object
+// (src/osqp_solver.py:38-40 setup, :137-143 update(Px), update(Ax), update(q, l, u), solve()).
+// oracle/osqp_admm.py restates OSQP and is pinned by the notebook's printed closed loop (the
+// first 12 goal distances of notebooks/pin_mpc_indy7.ipynb cell 2 to 1e-9); the C++ port
+// (oracle/cpp/i7m_cpu.cpp, Solver::admm) runs it in the block form this kernel runs.
+//
+// k_admm: one wavefront per problem, the whole QP in one launch:
+//   1. OSQP's Ruiz equilibration (10 passes) of [P A'; A 0] with the previous QP's q (the
+//      reference re-scales inside update(Ax), before update(q)), then the new q = c D g and
+//      l = u = E l;
+//   2. the x-update's matrix M = P + sigma I + A' diag(rho) A, block tridiagonal (18 x 18 blocks
+//      per knot (x_k, u_k), 12 x 18 couplings x_{k+1} <- z_k), factored by a block Cholesky
+//      whose diagonal factors are kept inverted (Linv_k) and whose couplings C_k = M_{k+1,k}
+//      Linv_k' are kept, so every solve is two sweeps of mat-vecs;
+//   3. OSQP's iteration from the problem's warm start (x, z, y, rho carried in HBM from call to
+//      call like the reference's OSQP object): the solve, relaxation alpha, projection onto
+//      [l, u], dual update; every `check` iterations the unscaled residuals and (OSQP 1.x) the
+//      duality gap; optional adaptive rho with a refactorisation.
+// Every row of A is an equality row (l = u), so rho_vec = 1e3 rho (RHO_EQ_OVER_RHO_INEQ).
+// Per-stage blocks live in HBM (Linv 324, C 216, scaled J 216 doubles) and are staged through
+// LDS per stage; the sweeps are bound by those reads.
+#pragma once
+
+#include "i7m_kernels.h"
+
+namespace i7m {
+
+struct AdmmCfg {
+  double rho0, sigma, alpha, eps_abs, eps_rel, adapt_tol;
+  int max_iter, check, scaling, gap, adapt_interval, pad;
+};
+
+struct AdmmArgs {
+  SolveParams P;
+  AdmmCfg A;
+  const double* lin;   // (B, N-1, 114) k_linearize
+  const double* cost;  // (B, N, 10)
+  const double* qpd;   // (B, N-1, 32): c_v
+  const double* xu;    // (B, T) linearisation point
+  const double* xs;    // (B, 12)
+  const int* active;
+  double* sol;         // (B, T) out: D x
+  // OSQP state per problem (scaled x, z, y; the previous QP's q, unscaled; rho)
+  double *sx, *sz, *sy, *sq, *srho;
+  // scratch per problem
+  double *Pq, *Pd, *J, *I, *qs, *ls, *D, *E, *Dt, *Et, *Linv, *C, *w, *xt;
+  int* iters;  // (B, I7M_MAX_SQP): OSQP iterations of SQP iteration `sqp_iter`
+  int sqp_iter;
+};
+
+__device__ __forceinline__ double adm_wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ double adm_wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double adm_limit(double v) { return v < 1e-4 ? 1.0 : (v > 1e4 ? 1e4 : v); }
+
+// unscaled J_k = [[I, dt I, 0], [Aq, Av, Bu]] (rows of A's block k+1 on z_k; src/osqp_solver.py:
+// 42-43, 70-81), from the linearisation record
+__device__ __forceinline__ double adm_jk(const double* L, double dt, int i, int j) {
+  if (i < 6) return j == i ? 1.0 : (j == 6 + i ? dt : 0.0);
+  const int r = i - 6;
+  return j < 6 ? L[6 * r + j] : (j < 12 ? L[36 + 6 * r + j - 6] : L[72 + 6 * r + j - 12]);
+}
+
+// coalesced copy of n doubles global -> LDS by the wave
+__device__ __forceinline__ void adm_stage(double* dst, const double* src, int n, int l) {
+  for (int e = l; e < n; e += 64) dst[e] = src[e];
+}
+
+// OSQP's check_termination on the unscaled residuals (+ the duality gap) and, for adapt_rho,
+// the scaled residual ratios; x, z, y scaled.  Returns solved; rho_est gets the estimate.
+__device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, double rho, const double* x,
+                          const double* z, const double* y, const double* qs, const double* ls, const double* D,
+                          const double* E, const double* Jb, const double* Ib, const double* Pq, const double* Pd,
+                          double* rho_est, int l) {
+  double pr = 0.0, zn = 0.0, an = 0.0, pri = 0.0, pn = 0.0;
+  double dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0, dua = 0.0, dn = 0.0, xPx = 0.0, qx = 0.0, sc = 0.0;
+  // rows: block 0 = I x_0, block k+1 = J_k z_k + I x_{k+1}
+  for (int r = l; r < m; r += 64) {
+    const int k = r / 12, i = r - 12 * k;
+    double ax;
+    if (k == 0) {
+      ax = Ib[r] * x[i];
+    } else {
+      const double* G = Jb + 216 * (k - 1) + 18 * i;
+      const double* xk = x + 18 * (k - 1);
+      double acc = 0.0;
+      for (int j = 0; j < 18; ++j) acc += G[j] * xk[j];
+      ax = acc + Ib[r] * x[18 * k + i];
+    }
+    const double ei = 1.0 / E[r];
+    pr = fmax(pr, fabs(ei * (ax - z[r])));
+    zn = fmax(zn, fabs(ei * z[r]));
+    an = fmax(an, fabs(ei * ax));
+    pri = fmax(pri, fabs(ax - z[r]));
+    pn = fmax(pn, fmax(fabs(z[r]), fabs(ax)));
+    sc += ls[r] * fmax(y[r], 0.0) + ls[r] * fmin(y[r], 0.0);
+  }
+  for (int e = l; e < T; e += 64) {
+    const int k = e / 18, j = e - 18 * k;
+    double px;
+    if (j < 6) {
+      double acc = 0.0;
+      for (int jj = 0; jj < 6; ++jj) acc += Pq[36 * k + 6 * j + jj] * x[18 * k + jj];
+      px = acc;
+    } else {
+      px = Pd[e] * x[e];
+    }
+    double aty = j < 12 ? Ib[12 * k + j] * y[12 * k + j] : 0.0;
+    if (k < N - 1) {
+      const double* G = Jb + 216 * k + j;
+      for (int i = 0; i < 12; ++i) aty += G[18 * i] * y[12 * (k + 1) + i];
+    }
+    const double di = 1.0 / D[e];
+    dr = fmax(dr, fabs(di * ((qs[e] + px) + aty)));
+    qn = fmax(qn, fabs(di * qs[e]));
+    atn = fmax(atn, fabs(di * aty));
+    pxn = fmax(pxn, fabs(di * px));
+    dua = fmax(dua, fabs(qs[e] + px + aty));
+    dn = fmax(dn, fmax(fabs(qs[e]), fmax(fabs(aty), fabs(px))));
+    xPx += x[e] * px;
+    qx += qs[e] * x[e];
+  }
+  pr = adm_wave_max(pr); zn = adm_wave_max(zn); an = adm_wave_max(an); pri = adm_wave_max(pri); pn = adm_wave_max(pn);
+  dr = adm_wave_max(dr); qn = adm_wave_max(qn); atn = adm_wave_max(atn); pxn = adm_wave_max(pxn);
+  dua = adm_wave_max(dua); dn = adm_wave_max(dn);
+  xPx = adm_wave_sum(xPx); qx = adm_wave_sum(qx); sc = adm_wave_sum(sc);
+  const double cinv = 1.0 / c;
+  // OSQP compute_rho_estimate (scaled residuals)
+  {
+    const double p = pri / (pn + 1e-30), d = dua / (dn + 1e-30);
+    double rn = rho * sqrt(p / (d + 1e-30));
+    *rho_est = fmin(fmax(rn, 1e-6), 1e6);
+  }
+  dr *= cinv;
+  if (!(pr < a.A.eps_abs + a.A.eps_rel * fmax(zn, an))) return false;
+  if (!(dr < a.A.eps_abs + a.A.eps_rel * cinv * fmax(qn, fmax(atn, pxn)))) return false;
+  if (a.A.gap) {
+    xPx *= cinv; qx *= cinv; sc *= cinv;
+    const double gp = xPx + qx + sc;
+    if (!(fabs(gp) < a.A.eps_abs + a.A.eps_rel * fmax(fabs(xPx), fmax(fabs(qx), fabs(sc))))) return false;
+  }
+  return true;
+}
+
+// M = P + sigma I + A' rho A, block Cholesky with inverted diagonal factors (as Solver::
+// admm_factor of the port): Linv (N, 18 x 18) and C (N-1, 12 x 18) to HBM
+__device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
+                           const double* Jb, double* Linv, double* Cb, double* sS, double* sJ, double* sL, double* sCp,
+                           int l) {
+  const double re = 1e3 * rho, sigma = a.A.sigma;
+  for (int k = 0; k < N; ++k) {
+    const int nk = k < N - 1 ? 18 : 12;
+    if (k < N - 1) adm_stage(sJ, Jb + 216 * k, 216, l);
+    wave_sync();
+    for (int e = l; e < 324; e += 64) {
+      const int i = e / 18, j = e - 18 * i;
+      double v = 0.0;
+      if (i < nk && j < nk) {
+        if (i < 6 && j < 6) v = Pq[36 * k + 6 * i + j];
+        else if (i == j && i >= 6) v = Pd[18 * k + i];
+        if (i == j) v += sigma;
+        if (i == j && i < 12) v += re * (Ib[12 * k + i] * Ib[12 * k + i]);
+        if (k < N - 1) {
+          double acc = 0.0;
+          for (int r = 0; r < 12; ++r) acc += sJ[18 * r + i] * sJ[18 * r + j];
+          v += re * acc;
+        }
+        if (k > 0 && i < 12 && j < 12) {
+          double acc = 0.0;
+          for (int q = 0; q < 18; ++q) acc += sCp[18 * i + q] * sCp[18 * j + q];
+          v -= acc;
+        }
+      }
+      sS[e] = v;
+    }
+    wave_sync();
+    // right-looking Cholesky
+    for (int p = 0; p < nk; ++p) {
+      const double d = sqrt(sS[18 * p + p]);
+      const double id = 1.0 / d;
+      wave_sync();
+      if (l == 0) sS[18 * p + p] = d;
+      if (l > p && l < nk) sS[18 * l + p] = sS[18 * l + p] * id;
+      wave_sync();
+      for (int e = l; e < 324; e += 64) {
+        const int i = e / 18, j = e - 18 * i;
+        if (j > p && i >= j && i < nk) sS[e] = sS[e] - sS[18 * i + p] * sS[18 * j + p];
+      }
+      wave_sync();
+    }
+    // inverse of the lower factor, one column per lane
+    for (int e = l; e < 324; e += 64) sL[e] = 0.0;
+    wave_sync();
+    if (l < nk) {
+      const int j = l;
+      sL[18 * j + j] = 1.0 / sS[18 * j + j];
+      for (int i = j + 1; i < nk; ++i) {
+        double acc = 0.0;
+        for (int q = j; q < i; ++q) acc += sS[18 * i + q] * sL[18 * q + j];
+        sL[18 * i + j] = -acc / sS[18 * i + i];
+      }
+    }
+    wave_sync();
+    for (int e = l; e < 324; e += 64) Linv[324 * k + e] = sL[e];
+    if (k < N - 1) {
+      for (int e = l; e < 216; e += 64) {
+        const int i = e / 18, j = e - 18 * i;
+        double acc = 0.0;
+        for (int q = 0; q <= j; ++q) acc += sJ[18 * i + q] * sL[18 * j + q];
+        const double cv = re * Ib[12 * (k + 1) + i] * acc;
+        sCp[e] = cv;
+        Cb[216 * k + e] = cv;
+      }
+    }
+    wave_sync_all();
+  }
+}
+
+__global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
+  const int b = blockIdx.x;
+  const SolveParams& P = a.P;
+  if (b >= P.B || (a.active && !a.active[b])) return;
+  const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
+  __shared__ double sL[324], sC[216], sJ[216], sS[324], sCp[216], sR[32], sW[32], sT0[16], sT1[16];
+  const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
+  const double* CO = a.cost + (long)b * N * COST_STRIDE;
+  const double* QD = a.qpd + (long)b * (N - 1) * QPD_STRIDE;
+  const double* X = a.xu + (long)b * T;
+  double* x = a.sx + (long)b * T;
+  double* z = a.sz + (long)b * m;
+  double* y = a.sy + (long)b * m;
+  double* qold = a.sq + (long)b * T;
+  double* Pq = a.Pq + (long)b * N * 36;
+  double* Pd = a.Pd + (long)b * T;
+  double* Jb = a.J + (long)b * (N - 1) * 216;
+  double* Ib = a.I + (long)b * m;
+  double* qs = a.qs + (long)b * T;
+  double* ls = a.ls + (long)b * m;
+  double* D = a.D + (long)b * T;
+  double* E = a.E + (long)b * m;
+  double* Dt = a.Dt + (long)b * T;
+  double* Et = a.Et + (long)b * m;
+  double* Linv = a.Linv + (long)b * N * 324;
+  double* Cb = a.C + (long)b * (N - 1) * 216;
+  double* wv = a.w + (long)b * T;
+  double* xt = a.xt + (long)b * T;
+  const double dt = P.dt;
+
+  // ---- 1. unscaled P blocks (src/osqp_solver.py:103-135), the previous q, D = E = 1
+  for (int k = 0; k < N; ++k) {
+    const double* w = CO + COST_STRIDE * k;
+    if (l < 36) Pq[36 * k + l] = w[6] * (w[l / 6] * w[l % 6]);
+    if (l < 18 && 18 * k + l < T) Pd[18 * k + l] = l < 6 ? 0.0 : (l < 12 ? w[7] : w[8]);
+  }
+  for (int e = l; e < T; e += 64) { qs[e] = qold[e]; D[e] = 1.0; }
+  for (int r = l; r < m; r += 64) E[r] = 1.0;
+  wave_sync_all();
+  double c = 1.0;
+  for (int pass = 0; pass < a.A.scaling; ++pass) {
+    // column inf-norms of the scaled [P; A] and row inf-norms of the scaled A
+    for (int k = 0; k < N; ++k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      const double* L = LIN + LIN_STRIDE * k;
+      if (l < nk) {
+        const int j = l, e = 18 * k + j;
+        const double dj = D[e];
+        double mx = 0.0;
+        if (j < 6) {
+          for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(Pq[36 * k + 6 * i + j]) * (D[18 * k + i] * dj) * c);
+        } else {
+          mx = fabs(Pd[e]) * (dj * dj) * c;
+        }
+        if (j < 12) mx = fmax(mx, E[12 * k + j] * dj);
+        if (k < N - 1)
+          for (int i = 0; i < 12; ++i) mx = fmax(mx, E[12 * (k + 1) + i] * fabs(adm_jk(L, dt, i, j)) * dj);
+        Dt[e] = 1.0 / sqrt(adm_limit(mx));
+      } else if (l >= 32 && l < 44 && k < N - 1) {
+        const int i = l - 32, r = 12 * (k + 1) + i;
+        const double er = E[r];
+        double mx = er * D[18 * (k + 1) + i];
+        for (int j = 0; j < 18; ++j) mx = fmax(mx, er * fabs(adm_jk(L, dt, i, j)) * D[18 * k + j]);
+        Et[r] = 1.0 / sqrt(adm_limit(mx));
+      } else if (l >= 48 && l < 60 && k == 0) {
+        const int i = l - 48;
+        Et[i] = 1.0 / sqrt(adm_limit(E[i] * D[i]));
+      }
+    }
+    wave_sync_all();
+    for (int e = l; e < T; e += 64) { D[e] = D[e] * Dt[e]; qs[e] = Dt[e] * qs[e]; }
+    for (int r = l; r < m; r += 64) E[r] = E[r] * Et[r];
+    wave_sync_all();
+    // cost normalisation: mean column norm of the scaled P, |q|
+    double s = 0.0, qm = 0.0;
+    for (int e = l; e < T; e += 64) {
+      const int k = e / 18, j = e - 18 * k;
+      double mx;
+      if (j < 6) {
+        mx = 0.0;
+        for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(Pq[36 * k + 6 * i + j]) * (D[18 * k + i] * D[e]) * c);
+      } else {
+        mx = fabs(Pd[e]) * (D[e] * D[e]) * c;
+      }
+      s += mx;
+      qm = fmax(qm, fabs(qs[e]));
+    }
+    s = adm_wave_sum(s);
+    qm = adm_limit(adm_wave_max(qm));
+    const double ct = 1.0 / adm_limit(fmax(s / T, qm));
+    for (int e = l; e < T; e += 64) qs[e] = qs[e] * ct;
+    c = c * ct;
+    wave_sync_all();
+  }
+  // scaled data: P <- c D P D, J <- E J D, I <- -E D, q <- c D g (update(q)), l <- E l
+  for (int k = 0; k < N; ++k) {
+    if (l < 36) {
+      const int i = l / 6, j = l % 6;
+      Pq[36 * k + l] = Pq[36 * k + l] * (D[18 * k + i] * D[18 * k + j]) * c;
+    }
+    if (l >= 6 && l < 18 && 18 * k + l < T) {
+      const int e = 18 * k + l;
+      Pd[e] = Pd[e] * (D[e] * D[e]) * c;
+    }
+    if (k < N - 1) {
+      const double* L = LIN + LIN_STRIDE * k;
+      for (int e = l; e < 216; e += 64) {
+        const int i = e / 18, j = e - 18 * i;
+        Jb[216 * k + e] = E[12 * (k + 1) + i] * adm_jk(L, dt, i, j) * D[18 * k + j];
+      }
+    }
+  }
+  for (int r = l; r < m; r += 64) {
+    const int k = r / 12, i = r - 12 * k;
+    Ib[r] = -E[r] * D[18 * k + i];
+    double lv;
+    if (k == 0) lv = -a.xs[12 * (long)b + i];
+    else lv = i < 6 ? 0.0 : -QD[QPD_STRIDE * (k - 1) + QPD_CV + i - 6];
+    ls[r] = E[r] * lv;
+  }
+  for (int e = l; e < T; e += 64) {
+    const int k = e / 18, j = e - 18 * k;
+    const double* w = CO + COST_STRIDE * k;
+    const double g = j < 6 ? w[6] * w[j] : (j < 12 ? w[7] * X[e] : w[8] * X[e]);
+    qold[e] = g;
+    qs[e] = c * (D[e] * g);
+  }
+  wave_sync_all();
+
+  // ---- 2. factor
+  double rho = a.srho[b];
+  adm_factor(a, N, rho, Pq, Pd, Ib, Jb, Linv, Cb, sS, sJ, sL, sCp, l);
+  double rv = 1e3 * rho, ri = 1.0 / rv;
+  const double al = a.A.alpha, sg = a.A.sigma;
+
+  // ---- 3. OSQP iterations
+  int it;
+  bool solved = false;
+  for (it = 1; it <= a.A.max_iter; ++it) {
+    // forward sweep: w_k = Linv_k (rhs_k - C_{k-1} w_{k-1})
+    if (l < 12) sT0[l] = rv * (z[l] - ri * y[l]);
+    for (int k = 0; k < N; ++k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      adm_stage(sL, Linv + 324 * k, 324, l);
+      if (k > 0) adm_stage(sC, Cb + 216 * (k - 1), 216, l);
+      if (k < N - 1) {
+        adm_stage(sJ, Jb + 216 * k, 216, l);
+        if (l < 12) {
+          const int r = 12 * (k + 1) + l;
+          sT1[l] = rv * (z[r] - ri * y[r]);
+        }
+      }
+      wave_sync();
+      if (l < nk) {
+        const int j = l, e = 18 * k + j;
+        double acc = j < 12 ? Ib[12 * k + j] * sT0[j] : 0.0;
+        if (k < N - 1)
+          for (int i = 0; i < 12; ++i) acc += sJ[18 * i + j] * sT1[i];
+        double r = (sg * x[e] - qs[e]) + acc;
+        if (k > 0 && j < 12) {
+          double cw = 0.0;
+          for (int q = 0; q < 18; ++q) cw += sC[18 * j + q] * sW[q];
+          r -= cw;
+        }
+        sR[j] = r;
+      }
+      wave_sync();
+      double wk = 0.0;
+      if (l < nk) {
+        for (int j = 0; j <= l; ++j) wk += sL[18 * l + j] * sR[j];
+        wv[18 * k + l] = wk;
+      }
+      wave_sync();
+      if (l < nk) sW[l] = wk;
+      if (l < 12) sT0[l] = sT1[l];
+      wave_sync();
+    }
+    wave_sync_all();
+    // backward sweep: xt_k = Linv_k' (w_k - C_k' xt_{k+1}); then A xt for the rows of block k+1,
+    // relaxation and projection of block k+1 (block 0 at the end)
+    for (int k = N - 1; k >= 0; --k) {
+      const int nk = k < N - 1 ? 18 : 12;
+      adm_stage(sL, Linv + 324 * k, 324, l);
+      if (k < N - 1) {
+        adm_stage(sC, Cb + 216 * k, 216, l);
+        adm_stage(sJ, Jb + 216 * k, 216, l);
+      }
+      wave_sync();
+      if (l < nk) {
+        double r = wv[18 * k + l];
+        if (k < N - 1) {
+          double acc = 0.0;
+          for (int q = 0; q < 12; ++q) acc += sC[18 * q + l] * sW[q];
+          r -= acc;
+        }
+        sR[l] = r;
+      }
+      wave_sync();
+      double xk = 0.0;
+      if (l < nk) {
+        for (int i = l; i < nk; ++i) xk += sL[18 * i + l] * sR[i];
+      }
+      // sW holds xt_{k+1}'s x part until block k+1's rows are done
+      if (l < nk) sR[l] = xk;  // (reuse: xt_k)
+      wave_sync();
+      if (k < N - 1 && l < 12) {
+        const int r = 12 * (k + 1) + l;
+        double acc = 0.0;
+        for (int j = 0; j < 18; ++j) acc += sJ[18 * l + j] * sR[j];
+        const double zt = acc + Ib[r] * sW[l];
+        const double zr = al * zt + (1.0 - al) * z[r];
+        double zn = zr + ri * y[r];
+        zn = fmin(fmax(zn, ls[r]), ls[r]);
+        y[r] = y[r] + rv * (zr - zn);
+        z[r] = zn;
+      }
+      if (k < N - 1) {
+        const int nn = k + 1 < N - 1 ? 18 : 12;
+        if (l < nn) {
+          const int e = 18 * (k + 1) + l;
+          x[e] = al * xt[e] + (1.0 - al) * x[e];
+        }
+      }
+      if (l < nk) xt[18 * k + l] = xk;
+      wave_sync_all();
+      if (l < 12) sW[l] = sR[l];
+      wave_sync();
+    }
+    // block 0 rows and x_0
+    if (l < 12) {
+      const double zt = Ib[l] * sW[l];
+      const double zr = al * zt + (1.0 - al) * z[l];
+      double zn = zr + ri * y[l];
+      zn = fmin(fmax(zn, ls[l]), ls[l]);
+      y[l] = y[l] + rv * (zr - zn);
+      z[l] = zn;
+    }
+    if (l < 18) x[l] = al * xt[l] + (1.0 - al) * x[l];
+    wave_sync_all();
+    const bool chk = a.A.check && it % a.A.check == 0;
+    const bool adapt = a.A.adapt_interval && it % a.A.adapt_interval == 0;
+    if (chk || adapt) {
+      double rest = rho;
+      const bool ok = adm_check(a, N, T, m, c, rho, x, z, y, qs, ls, D, E, Jb, Ib, Pq, Pd, &rest, l);
+      if (chk && ok) {
+        solved = true;
+        break;
+      }
+      if (adapt && (rest > rho * a.A.adapt_tol || rest < rho / a.A.adapt_tol)) {
+        rho = rest;
+        rv = 1e3 * rho;
+        ri = 1.0 / rv;
+        adm_factor(a, N, rho, Pq, Pd, Ib, Jb, Linv, Cb, sS, sJ, sL, sCp, l);
+      }
+    }
+  }
+  (void)solved;
+  if (l == 0) {
+    a.srho[b] = rho;
+    if (a.iters) a.iters[(long)b * 8 + a.sqp_iter] = it > a.A.max_iter ? a.A.max_iter : it;
+  }
+  double* so = a.sol + (long)b * T;
+  for (int e = l; e < T; e += 64) so[e] = D[e] * x[e];
+}
+
+}  // namespace i7m

@@ -22,6 +22,7 @@
 #include "i7m_linearize.h"
 #include "i7m_riccati_mfma.h"
 #include "i7m_box.h"
+#include "i7m_admm.h"
 #include "i7m_mpc.h"
 
 // Source hash of the tree this library was built from (__graft_entry__.build passes it), so
@@ -104,6 +105,9 @@ struct i7m_handle {
   double *d_bhinv = nullptr, *d_bdh = nullptr;  // per-stage H^-1 (max_batch, N-1, 36); corrector dh (max_batch, T)
   IpmState* d_bst = nullptr;
   int* d_bact = nullptr;
+  // I7M_QP_ADMM (i7m_admm.h): one allocation, per-problem OSQP state and k_admm scratch
+  double* d_admm = nullptr;
+  int* d_admm_it = nullptr;  // (max_batch, I7M_MAX_SQP) OSQP iterations per SQP iteration
   // box QP: 1 k_ipm_fused<false> (default), 0 I7M_IPM=delta (k_ipm_fused<true>: the corrector
   // reuses the predictor's factorisation; measured slower), 2 I7M_IPM=split
   int ipm_mode = 1;
@@ -251,7 +255,44 @@ struct Bufs {
   double *bx, *bzl, *bzu, *bsig, *bh, *bdxa, *bhinv, *bdh;
   IpmState* bst;
   int* bact;
+  // ADMM mode only: AdmmArgs' per-problem pointers for this range (P, A, sqp_iter filled at launch)
+  AdmmArgs adm;
 };
+
+// per-problem sizes of the ADMM buffers (doubles), in the order admm_layout lays them out
+constexpr int ADM_NBUF = 19;
+void admm_sizes(long N, long sz[ADM_NBUF]) {
+  const long T = 18 * N - 6, m = 12 * N;
+  const long v[ADM_NBUF] = {T, m, m, T, 1,                                  // x z y q rho (state)
+                            36 * N, T, 216 * (N - 1), m, T, m, T, m, T, m,  // Pq Pd J I qs ls D E Dt Et
+                            324 * N, 216 * (N - 1), T, T};                  // Linv C w xt
+  for (int i = 0; i < ADM_NBUF; ++i) sz[i] = v[i];
+}
+// AdmmArgs pointers of problems [b0, ...) in the handle's ADMM allocation (array-of-buffers, each
+// (max_batch, size) row-major)
+AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
+  long sz[ADM_NBUF];
+  admm_sizes(N, sz);
+  double* p[ADM_NBUF];
+  double* cur = base;
+  for (int i = 0; i < ADM_NBUF; ++i) {
+    p[i] = cur + b0 * sz[i];
+    cur += Bm * sz[i];
+  }
+  AdmmArgs a{};
+  a.sx = p[0]; a.sz = p[1]; a.sy = p[2]; a.sq = p[3]; a.srho = p[4];
+  a.Pq = p[5]; a.Pd = p[6]; a.J = p[7]; a.I = p[8]; a.qs = p[9]; a.ls = p[10]; a.D = p[11]; a.E = p[12];
+  a.Dt = p[13]; a.Et = p[14]; a.Linv = p[15]; a.C = p[16]; a.w = p[17]; a.xt = p[18];
+  a.iters = its + b0 * I7M_MAX_SQP;
+  return a;
+}
+size_t admm_doubles(long Bm, long N) {
+  long sz[ADM_NBUF];
+  admm_sizes(N, sz);
+  size_t t = 0;
+  for (int i = 0; i < ADM_NBUF; ++i) t += (size_t)(Bm * sz[i]);
+  return t;
+}
 
 Bufs bufs_at(const i7m_handle* h, long b0) {
   const long N = h->cfg.N, T = 18 * N - 6;
@@ -270,7 +311,24 @@ Bufs bufs_at(const i7m_handle* h, long b0) {
     W.bst = h->d_bst + b0;
     W.bact = h->d_bact + b0;
   }
+  if (h->cfg.qp_mode == I7M_QP_ADMM) W.adm = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, N, b0);
   return W;
+}
+
+AdmmCfg admm_cfg_of(const i7m_config& c) {
+  AdmmCfg A{};
+  A.rho0 = c.admm_rho;
+  A.sigma = c.admm_sigma;
+  A.alpha = c.admm_alpha;
+  A.eps_abs = c.admm_eps_abs;
+  A.eps_rel = c.admm_eps_rel;
+  A.adapt_tol = c.admm_adaptive_rho_tolerance;
+  A.max_iter = c.admm_max_iter;
+  A.check = c.admm_check_termination;
+  A.scaling = c.admm_scaling;
+  A.gap = c.admm_check_dualgap;
+  A.adapt_interval = c.admm_adaptive_rho_interval;
+  return A;
 }
 
 // init_active / init_stats (first SQP iteration only): the kernel marks every problem active
@@ -442,8 +500,27 @@ BoxParams box_params(const i7m_handle* h) {
 // box mode the interior-point iteration started from it (i7m_box.h; oracle/box_ipm.py).
 // Returns where the minimiser is: `sol`, or W.bx in box mode.
 int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, const double* xu, const double* xs,
-             const int* active, double* sol, const double** out) {
+             const int* active, double* sol, const double** out, int sqp_iter = 0) {
   int rc;
+  if (h->cfg.qp_mode == I7M_QP_ADMM) {
+    // OSQP's iteration from the problems' carried state (i7m_admm.h; oracle/osqp_admm.py)
+    *out = sol;
+    if (P.B == 0) return I7M_OK;
+    AdmmArgs a = W.adm;
+    a.P = P;
+    a.A = admm_cfg_of(h->cfg);
+    a.lin = W.lin;
+    a.cost = W.cost;
+    a.qpd = W.qpd;
+    a.xu = xu;
+    a.xs = xs;
+    a.active = active;
+    a.sol = sol;
+    a.sqp_iter = sqp_iter;
+    return timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
+      hipExtLaunchKernelGGL(k_admm, dim3(P.B), dim3(64), 0, s, ea, eb, 0, a);
+    });
+  }
   if ((rc = launch_riccati(h, s, W, P, xu, xs, active, sol))) return rc;
   *out = sol;
   if (h->cfg.qp_mode != I7M_QP_BOX || P.B == 0) return I7M_OK;
@@ -541,7 +618,7 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
       rc = launch_linearize(h, s, W, P, xin, d_goals, act);
     if (rc) return rc;
     const double* qsol = nullptr;
-    if ((rc = solve_qp(h, s, W, P, xin, d_xs, act, qbuf, &qsol))) return rc;
+    if ((rc = solve_qp(h, s, W, P, xin, d_xs, act, qbuf, &qsol, it))) return rc;
     if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, act, d_st, nullptr, it, 0,
                                 h->ablate != 6)))
       return rc;
@@ -843,6 +920,19 @@ int i7m_config_default(i7m_config* c) {
   c->box_mask = I7M_BOX_Q | I7M_BOX_V | I7M_BOX_U;
   c->box_max_iters = 30;
   c->box_tol = 1e-8;
+  // OSQP's defaults, with the duality-gap test and no rho adaptation: the settings that reproduce
+  // the reference's printed closed loop (oracle/osqp_admm.py)
+  c->admm_rho = 0.1;
+  c->admm_sigma = 1e-6;
+  c->admm_alpha = 1.6;
+  c->admm_eps_abs = 1e-3;
+  c->admm_eps_rel = 1e-3;
+  c->admm_max_iter = 4000;
+  c->admm_check_termination = 25;
+  c->admm_scaling = 10;
+  c->admm_check_dualgap = 1;
+  c->admm_adaptive_rho_interval = 0;
+  c->admm_adaptive_rho_tolerance = 5.0;
   return I7M_OK;
 }
 
@@ -852,7 +942,18 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (cfg->N < 2 || cfg->N > I7M_MAX_N) return fail(I7M_EINVAL, "N must be in [2, 64]");
   if (cfg->max_batch < 1) return fail(I7M_EINVAL, "max_batch must be >= 1");
   if (cfg->max_sqp_iters < 1 || cfg->max_sqp_iters > I7M_MAX_SQP) return fail(I7M_EINVAL, "max_sqp_iters in [1, 8]");
-  if (cfg->qp_mode != I7M_QP_DIRECT && cfg->qp_mode != I7M_QP_BOX) return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (cfg->qp_mode != I7M_QP_DIRECT && cfg->qp_mode != I7M_QP_BOX && cfg->qp_mode != I7M_QP_ADMM)
+    return fail(I7M_EINVAL, "unsupported qp_mode");
+  if (cfg->qp_mode == I7M_QP_ADMM) {
+    if (!(cfg->admm_rho > 0.0) || !(cfg->admm_sigma > 0.0)) return fail(I7M_EINVAL, "admm_rho and admm_sigma must be > 0");
+    if (!(cfg->admm_alpha > 0.0 && cfg->admm_alpha < 2.0)) return fail(I7M_EINVAL, "admm_alpha must be in (0, 2)");
+    if (!(cfg->admm_eps_abs >= 0.0) || !(cfg->admm_eps_rel >= 0.0)) return fail(I7M_EINVAL, "admm eps must be >= 0");
+    if (cfg->admm_max_iter < 1 || cfg->admm_max_iter > 1000000) return fail(I7M_EINVAL, "admm_max_iter in [1, 1e6]");
+    if (cfg->admm_check_termination < 0 || cfg->admm_scaling < 0 || cfg->admm_scaling > 100 ||
+        cfg->admm_adaptive_rho_interval < 0)
+      return fail(I7M_EINVAL, "admm_check_termination / admm_adaptive_rho_interval >= 0, admm_scaling in [0, 100]");
+    if (!(cfg->admm_adaptive_rho_tolerance >= 1.0)) return fail(I7M_EINVAL, "admm_adaptive_rho_tolerance must be >= 1");
+  }
   if (cfg->pipeline < I7M_PIPE_AUTO || cfg->pipeline > I7M_PIPE_FUSED_ITER) return fail(I7M_EINVAL, "unsupported pipeline");
   if (cfg->qp_mode == I7M_QP_BOX) {
     if (cfg->box_mask < 0 || cfg->box_mask > 7) return fail(I7M_EINVAL, "box_mask must be a subset of Q|V|U (0..7)");
@@ -942,6 +1043,12 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
          alloc((void**)&h->d_bh, Bm * T * 8) && alloc((void**)&h->d_bdxa, Bm * T * 8) &&
          alloc((void**)&h->d_bhinv, Bm * (N - 1) * 36 * 8) && alloc((void**)&h->d_bdh, Bm * T * 8) &&
          alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
+  if (ok && cfg->qp_mode == I7M_QP_ADMM) {
+    ok = alloc((void**)&h->d_admm, admm_doubles((long)Bm, (long)N) * 8) &&
+         alloc((void**)&h->d_admm_it, Bm * I7M_MAX_SQP * sizeof(int));
+    h->cfg.qp_mode = I7M_QP_ADMM;
+    if (ok && i7m_admm_reset(h, cfg->max_batch, I7M_ADMM_RESET_ALL) != I7M_OK) ok = false;
+  }
   if (!ok) return bail(fail(I7M_ENOMEM, "hipMalloc failed for max_batch=" + std::to_string(cfg->max_batch)));
   DevModel dm = make_dev_model(cfg->model);
   // the Indy7-specialised kernels are used only for a model bit-identical to the baked one
@@ -960,7 +1067,7 @@ void i7m_destroy(i7m_handle* h) {
   void* bufs[] = {h->d_model, h->d_xu, h->d_xs, h->d_goal, h->d_sol, h->d_lin, h->d_cost,
                   h->d_kbuf, h->d_aux, h->d_out, h->d_active, h->d_stats, h->d_fext, h->d_qpd, h->d_lsbase, h->d_lspend,
                   h->d_bx, h->d_bzl, h->d_bzu, h->d_bsig, h->d_bh, h->d_bdxa, h->d_bst, h->d_bact,
-                  h->d_bhinv, h->d_bdh};
+                  h->d_bhinv, h->d_bdh, h->d_admm, h->d_admm_it};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (auto& t : h->ev) {
@@ -1019,7 +1126,66 @@ int i7m_reset(i7m_handle* h) {
   HIPCHK(hipSetDevice(h->dev));
   HIPCHK(hipStreamSynchronize(h->stream));
   drop_graphs(h);
+  if (h->cfg.qp_mode == I7M_QP_ADMM) {
+    const int rc = i7m_admm_reset(h, h->cfg.max_batch, I7M_ADMM_RESET_ALL);
+    if (rc) return rc;
+  }
   return i7m_reset_kernel_times(h);
+}
+
+int i7m_admm_reset(i7m_handle* h, int32_t B, int32_t what) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (h->cfg.qp_mode != I7M_QP_ADMM) return fail(I7M_EINVAL, "handle is not in I7M_QP_ADMM mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  if (what & ~I7M_ADMM_RESET_ALL) return fail(I7M_EINVAL, "unknown I7M_ADMM_RESET_* bits");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const long N = h->cfg.N, T = 18 * N - 6, m = 12 * N;
+  const AdmmArgs a = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, N, 0);
+  if (what & I7M_ADMM_RESET_PRIMAL) {
+    HIPCHK(hipMemsetAsync(a.sx, 0, (size_t)B * T * 8, h->stream));
+    HIPCHK(hipMemsetAsync(a.sz, 0, (size_t)B * m * 8, h->stream));
+    HIPCHK(hipMemsetAsync(a.sq, 0, (size_t)B * T * 8, h->stream));
+  }
+  if (what & I7M_ADMM_RESET_DUAL) HIPCHK(hipMemsetAsync(a.sy, 0, (size_t)B * m * 8, h->stream));
+  if (what & I7M_ADMM_RESET_RHO) {
+    std::vector<double> r((size_t)B, h->cfg.admm_rho);
+    HIPCHK(hipMemcpyAsync(a.srho, r.data(), (size_t)B * 8, hipMemcpyHostToDevice, h->stream));
+  }
+  HIPCHK(hipMemsetAsync(a.iters, 0xff, (size_t)B * I7M_MAX_SQP * sizeof(int), h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_get_admm_stats(i7m_handle* h, int32_t B, int32_t* iters, double* rho) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (h->cfg.qp_mode != I7M_QP_ADMM) return fail(I7M_EINVAL, "handle is not in I7M_QP_ADMM mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const AdmmArgs a = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, h->cfg.N, 0);
+  if (iters) HIPCHK(hipMemcpyAsync(iters, a.iters, (size_t)B * I7M_MAX_SQP * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  if (rho) HIPCHK(hipMemcpyAsync(rho, a.srho, (size_t)B * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_get_admm_state(i7m_handle* h, int32_t B, double* x, double* z, double* y, double* q, double* rho) {
+  if (!h) return fail(I7M_EINVAL, "null handle");
+  if (h->cfg.qp_mode != I7M_QP_ADMM) return fail(I7M_EINVAL, "handle is not in I7M_QP_ADMM mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const long N = h->cfg.N, T = 18 * N - 6, m = 12 * N;
+  const AdmmArgs a = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, N, 0);
+  int rc;
+  if (x && (rc = copy_out(h, x, a.sx, (size_t)B * T))) return rc;
+  if (z && (rc = copy_out(h, z, a.sz, (size_t)B * m))) return rc;
+  if (y && (rc = copy_out(h, y, a.sy, (size_t)B * m))) return rc;
+  if (q && (rc = copy_out(h, q, a.sq, (size_t)B * T))) return rc;
+  if (rho && (rc = copy_out(h, rho, a.srho, (size_t)B))) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
 }
 
 int i7m_synchronize(i7m_handle* h) {

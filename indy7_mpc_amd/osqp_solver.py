@@ -3,7 +3,11 @@
 Same constructor, attributes and methods.  The numbers come from the GPU:
   * ``setup_and_solve_qp`` linearises on the device (k_linearize) and solves the QP EXACTLY
     with the block-tridiagonal Riccati kernel (k_riccati).  The reference hands the same
-    P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.
+    P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.  With
+    ``qp_mode="admm"`` it runs OSQP's algorithm itself (k_admm, i7m_admm.h) from a warm-started
+    per-problem OSQP state, as the reference's ``self.osqp`` object does (:38-40, 140-143): the
+    trajectories are then the reference's own (oracle/osqp_admm.py pins them against the
+    notebook's printed closed loop).
   * ``Pdata/Adata/l/g`` (the CSC value arrays the reference fills, :95-135) are assembled on
     the host from the device linearisation, in the reference's exact value order.  The solve
     itself does not need them, so after ``setup_and_solve_qp`` they are filled lazily: the call
@@ -26,19 +30,25 @@ from . import _lib
 class QPSolution:
     """What ``osqp.OSQP().solve()`` returns, as far as the reference uses it (``.x``)."""
 
-    def __init__(self, x, status="solved"):
+    def __init__(self, x, status="solved", iters=0):
         self.x = x
         self.y = None
-        self.info = type("info", (), {"status": status, "iter": 0})()
+        self.info = type("info", (), {"status": status, "iter": iters})()
 
 
 class OSQPSolver:
     def __init__(self, model, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
                  max_batch=1, device_id=0, box_constraints=False, box_mask=_lib.BOX_Q | _lib.BOX_V | _lib.BOX_U,
-                 box_max_iters=30, box_tol=1e-8):
+                 box_max_iters=30, box_tol=1e-8, qp_mode="direct", admm=None):
         """Reference signature (src/osqp_solver.py:7) plus: max_batch / device_id (device
-        buffers), and the config-4 extension ``box_constraints``: box rows on
-        q, v, u from the model's URDF limits, solved by the interior-point mode (I7M_QP_BOX)."""
+        buffers); the config-4 extension ``box_constraints``: box rows on
+        q, v, u from the model's URDF limits, solved by the interior-point mode (I7M_QP_BOX);
+        ``qp_mode``: "direct" (exact KKT solve) or "admm" (OSQP's iteration with its carried
+        state; ``admm`` overrides OSQP settings, keys of _lib.ADMM_DEFAULTS)."""
+        if qp_mode not in ("direct", "admm"):
+            raise ValueError("qp_mode must be 'direct' or 'admm'")
+        if qp_mode == "admm" and box_constraints:
+            raise ValueError("box_constraints use the interior-point mode; qp_mode='admm' is the reference's equality QP")
         self.model = model
         self.data = model.createData()
         self.N = N
@@ -66,8 +76,9 @@ class OSQPSolver:
                                          np.ones((self.nq, 2 * self.nq))])])
         self.B_k = np.zeros((self.nx, self.nq))
         self.cx_k = np.zeros(self.nx)
-        self.box = dict(qp_mode=_lib.QP_BOX if box_constraints else _lib.QP_DIRECT, box_mask=box_mask,
-                        box_max_iters=box_max_iters, box_tol=box_tol)
+        mode = _lib.QP_ADMM if qp_mode == "admm" else (_lib.QP_BOX if box_constraints else _lib.QP_DIRECT)
+        # the QP-mode keyword arguments every handle of this solver is created with
+        self.box = dict(qp_mode=mode, box_mask=box_mask, box_max_iters=box_max_iters, box_tol=box_tol, admm=admm)
         self.handle = _lib.Handle(model, N=N, dt=dt, dQ_cost=dQ_cost, R_cost=R_cost, QN_cost=QN_cost,
                                   regularize=regularize, eps=eps, max_batch=max_batch, device_id=device_id, **self.box)
 
@@ -115,7 +126,9 @@ class OSQPSolver:
         """reference :137-143 — linearise at xu, solve the QP; returns an object with ``.x``.
         Pdata / Adata / l / g describe this QP afterwards (assembled on first read)."""
         xu, xs, eepos_g = (np.array(a, dtype=float) for a in (xu, xs, eepos_g))
-        sol = QPSolution(self.handle.qp(xu, xs, eepos_g)[0])
+        x = self.handle.qp(xu, xs, eepos_g)[0]
+        iters = int(self.handle.admm_stats(1)[0][0, 0]) if self.box["qp_mode"] == _lib.QP_ADMM else 0
+        sol = QPSolution(x, iters=iters)
         self._pending_A = (xu, xs)
         self._pending_P = (xu, eepos_g)
         return sol
