@@ -265,6 +265,119 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
     return res
 
 
+def admm_bytes_per_iter(N: int):
+    """HBM bytes one OSQP iteration of k_admm streams per problem (i7m_admm.h): the forward and the
+    backward sweep each read every stage's packed Linv (171), coupling C (216) and compact scaled J
+    (120) doubles, plus the per-knot vectors (x, q, z, y, w, xt and the scaling rows: ~120 doubles
+    per knot)."""
+    return 8 * (2 * (171 * N + 336 * (N - 1)) + 120 * N)
+
+
+def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 32, native=None,
+                 cpu_budget: float = 10.0, cpu_threads: int = 1):
+    """Config 3's problems (B = 4096, N = 32) with the QP solved by OSQP's own algorithm on the
+    device (I7M_QP_ADMM, k_admm) — the reference's solver (src/osqp_solver.py:38-40, 137-143).
+    Reported beside the headline (which solves each QP exactly).  Every timed step starts from a
+    fresh OSQP state (i7m_admm_reset outside the timed region, the step itself timed by HIP events
+    on the solve stream): the reference's first solve, its hardest.  With `native` (rank 0, N = 1)
+    it carries `parity_vs_port` (every problem of one cold step against the port's ADMM mode) and
+    `cpu_baseline` (the port's ADMM mode on a bounded sample)."""
+    import torch
+    from indy7_mpc_amd import _lib
+    from indy7_mpc_amd.synthetic import make_batch
+
+    dev = torch.device("cuda", local)
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=_lib.QP_ADMM)
+    h.set_stream(stream.cuda_stream)
+    xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 3)
+    t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
+    t_out = torch.empty_like(t_xu)
+    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+
+    def step():
+        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
+
+    h.admm_reset()
+    step()  # warm-up (kernel load)
+    torch.cuda.synchronize(dev)
+    times, its = [], []
+    h.reset_kernel_times()
+    h.set_timing(True)
+    for _ in range(steps):
+        h.admm_reset()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        times.append(a.elapsed_time(b) / 1e3)
+        its.append(h.admm_stats(B)[0])
+    h.set_timing(False)
+    kt = h.kernel_times()
+    out = t_out.cpu().numpy()
+    st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
+    it = its[-1]
+    h.close()
+    el = float(np.mean(times))
+    used = it[it >= 0]
+    res = {"workload": f"config3 ADMM: B={B}, N={N}, OSQP's iteration per QP (I7M_QP_ADMM), cold OSQP state each step",
+           "value": B / el, "unit": "solves/s", "ms_per_step": 1e3 * el, "steps": steps,
+           "osqp_iters_per_qp": {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())},
+           "qp_iters_mean": float(st["qp_iters"].mean()), "finite": bool(np.isfinite(out).all()),
+           "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
+    if "k_admm" in kt:
+        ms, cnt = kt["k_admm"]
+        avg_s = ms / max(cnt, 1) / 1e3
+        # problems per launch and OSQP iterations per launch (the last step's record)
+        ppl = float((it >= 0).sum()) / max(cnt // steps, 1)
+        ipl = float(used.sum()) / max(cnt // steps, 1)
+        ab = algorithmic_bytes(N)
+        achieved = ppl * ab / avg_s / 1e9
+        stream_gbs = ipl * admm_bytes_per_iter(N) / avg_s / 1e9
+        res["roofline"] = {"bound": "hbm", "kernel": "k_admm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic("k_admm", B, N),
+                           "algorithmic_bytes_per_problem": ab, "problems_per_launch": ppl,
+                           "avg_launch_us": avg_s * 1e6,
+                           "factor_stream": {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,
+                                             "achieved_GBs": stream_gbs, "frac": stream_gbs / HBM_PEAK_GBS,
+                                             "note": "the blocks every OSQP iteration re-reads (bench.admm_bytes_per_iter)"}}
+    if native is not None:
+        from oracle import cpu
+        lib_path, build_desc = native
+        cpu.load(lib_path)
+        stp = cpu.AdmmState(B, N)
+        ref, qp, al, _, rit = cpu.solve_admm(xcur, goals, XU, N, stp, nthreads=cpu_threads)
+        rel = np.linalg.norm(out - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
+        ga = st["alphas"][:, :al.shape[1]]
+        used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
+        used_c = ~np.isnan(al)
+        same_alpha = np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == al, True), axis=1)
+        same_it = np.all(np.where(rit >= 0, it == rit, True), axis=1)
+        res["parity_vs_port"] = {
+            "problems": int(B), "alpha_sequence_agreement": float(same_alpha.mean()),
+            "osqp_iters_agreement": float(same_it.mean()), "qp_iters_agreement": float((st["qp_iters"] == qp).mean()),
+            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
+            "reference": "oracle/cpp/i7m_cpu.cpp ADMM mode (oracle/osqp_admm.py in block form)"}
+        t0 = time.perf_counter()
+        cpu.solve_admm(xcur[:4], goals[:4], XU[:4], N, cpu.AdmmState(4, N), nthreads=1)
+        per = (time.perf_counter() - t0) / 4
+        n = int(max(4, min(B, cpu_budget / 2 / per)))
+        t0 = time.perf_counter()
+        cpu.solve_admm(xcur[:n], goals[:n], XU[:n], N, cpu.AdmmState(n, N), nthreads=1)
+        t1 = time.perf_counter()
+        nm = min(B, n * cpu_threads)
+        t2 = time.perf_counter()
+        cpu.solve_admm(xcur[:nm], goals[:nm], XU[:nm], N, cpu.AdmmState(nm, N), nthreads=cpu_threads)
+        t3 = time.perf_counter()
+        res["cpu_baseline"] = {
+            "value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{n} cold ADMM-mode solves (the first {n} of these draws) by oracle/cpp/i7m_cpu.cpp, 1 thread, "
+                      f"{t1 - t0:.1f}s",
+            "build": build_desc,
+            "all_cores": {"value": nm / (t3 - t2), "cores": cpu_threads, "sample": f"{nm} solves, {cpu_threads} threads"}}
+    return res
+
+
 def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: int = 32):
     """a small batch (B = 64, N = 32) on one GPU, device-resident inputs,
     same step definition as the headline.  At this size every kernel is one partially filled
@@ -395,6 +508,8 @@ def main():
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (box QP) extra object")
     ap.add_argument("--config4-steps", type=int, default=3)
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (B=64) extra object")
+    ap.add_argument("--no-admm", action="store_true", help="skip the config-3 ADMM-mode (OSQP) extra object")
+    ap.add_argument("--admm-steps", type=int, default=3)
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -561,6 +676,8 @@ def main():
     cpu = None if native is None else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads, native)
     c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1,
                                                             native=native, cpu_threads=args.cpu_threads)
+    ca = None if (args.no_admm or world > 1) else config3_admm(model, stream, local, args.admm_steps, B, N,
+                                                               native=native, cpu_threads=args.cpu_threads)
     c2 = None if (args.no_config2 or world > 1) else config2(model, stream, local, 200, 10)
     mpc = None if (args.no_config2 or world > 1) else mpc_closed_loop(model, stream, local, B, N)
     out = {
@@ -646,6 +763,8 @@ def main():
         out["config2"] = c2
     if c4 is not None:
         out["config4"] = c4
+    if ca is not None:
+        out["config3_admm"] = ca
     if mpc is not None:
         out["mpc_closed_loop"] = mpc
     print(json.dumps(out), flush=True)

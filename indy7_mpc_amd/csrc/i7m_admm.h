@@ -19,8 +19,8 @@
 //      [l, u], dual update; every `check` iterations the unscaled residuals and (OSQP 1.x) the
 //      duality gap; optional adaptive rho with a refactorisation.
 // Every row of A is an equality row (l = u), so rho_vec = 1e3 rho (RHO_EQ_OVER_RHO_INEQ).
-// Per-stage blocks live in HBM (Linv 324, C 216, scaled J 216 doubles) and are staged through
-// LDS per stage; the sweeps are bound by those reads.
+// Per-stage blocks live in HBM (Linv packed 171, C 216, scaled J compact 120 doubles) and are
+// staged through LDS per stage; the sweeps are bound by those reads.
 #pragma once
 
 #include "i7m_kernels.h"
@@ -48,7 +48,37 @@ struct AdmmArgs {
   double *Pq, *Pd, *J, *I, *qs, *ls, *D, *E, *Dt, *Et, *Linv, *C, *w, *xt;
   int* iters;  // (B, I7M_MAX_SQP): OSQP iterations of SQP iteration `sqp_iter`
   int sqp_iter;
+  int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
 };
+
+// HBM layout of the per-stage blocks (what every OSQP iteration streams): the inverted diagonal
+// factor packed lower-triangular (171 of 324), the scaled J_k as its q rows' two diagonals
+// (E_i D_i for I, E_i dt D_{6+i} for dt I) and its v rows (6 x 18): 120 of 216.  Staged to LDS
+// unpacked, so the arithmetic is the dense form's (the dropped entries are exact zeros).
+constexpr int ADM_LP = 171, ADM_JC = 120;
+__device__ __forceinline__ int adm_tri(int i, int j) { return i * (i + 1) / 2 + j; }
+// dense 12 x 18 J_k into LDS from its compact form
+__device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
+  for (int e = l; e < 216; e += 64) {
+    const int i = e / 18, j = e - 18 * i;
+    double v;
+    if (i < 6) v = j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
+    else v = Jc[12 + 18 * (i - 6) + j];
+    sJ[e] = v;
+  }
+}
+// dense 18 x 18 lower-triangular Linv into LDS from its packed form
+__device__ __forceinline__ void adm_stage_L(double* sL, const double* Lp, int l) {
+  for (int e = l; e < 324; e += 64) {
+    const int i = e / 18, j = e - 18 * i;
+    sL[e] = j <= i ? Lp[adm_tri(i, j)] : 0.0;
+  }
+}
+// entry (i, j) of the compact J_k in HBM
+__device__ __forceinline__ double adm_jc(const double* Jc, int i, int j) {
+  if (i < 6) return j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
+  return Jc[12 + 18 * (i - 6) + j];
+}
 
 __device__ __forceinline__ double adm_wave_max(double v) {
 #pragma unroll
@@ -90,10 +120,10 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     if (k == 0) {
       ax = Ib[r] * x[i];
     } else {
-      const double* G = Jb + 216 * (k - 1) + 18 * i;
+      const double* G = Jb + ADM_JC * (k - 1);
       const double* xk = x + 18 * (k - 1);
       double acc = 0.0;
-      for (int j = 0; j < 18; ++j) acc += G[j] * xk[j];
+      for (int j = 0; j < 18; ++j) acc += adm_jc(G, i, j) * xk[j];
       ax = acc + Ib[r] * x[18 * k + i];
     }
     const double ei = 1.0 / E[r];
@@ -116,8 +146,8 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     }
     double aty = j < 12 ? Ib[12 * k + j] * y[12 * k + j] : 0.0;
     if (k < N - 1) {
-      const double* G = Jb + 216 * k + j;
-      for (int i = 0; i < 12; ++i) aty += G[18 * i] * y[12 * (k + 1) + i];
+      const double* G = Jb + ADM_JC * k;
+      for (int i = 0; i < 12; ++i) aty += adm_jc(G, i, j) * y[12 * (k + 1) + i];
     }
     const double di = 1.0 / D[e];
     dr = fmax(dr, fabs(di * ((qs[e] + px) + aty)));
@@ -159,7 +189,7 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
   const double re = 1e3 * rho, sigma = a.A.sigma;
   for (int k = 0; k < N; ++k) {
     const int nk = k < N - 1 ? 18 : 12;
-    if (k < N - 1) adm_stage(sJ, Jb + 216 * k, 216, l);
+    if (k < N - 1) adm_stage_J(sJ, Jb + ADM_JC * k, l);
     wave_sync();
     for (int e = l; e < 324; e += 64) {
       const int i = e / 18, j = e - 18 * i;
@@ -210,7 +240,10 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
       }
     }
     wave_sync();
-    for (int e = l; e < 324; e += 64) Linv[324 * k + e] = sL[e];
+    for (int e = l; e < 324; e += 64) {
+      const int i = e / 18, j = e - 18 * i;
+      if (j <= i) Linv[ADM_LP * k + adm_tri(i, j)] = sL[e];
+    }
     if (k < N - 1) {
       for (int e = l; e < 216; e += 64) {
         const int i = e / 18, j = e - 18 * i;
@@ -226,7 +259,7 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
 }
 
 __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
-  const int b = blockIdx.x;
+  const int b = a.b0 + blockIdx.x;
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
@@ -241,7 +274,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   double* qold = a.sq + (long)b * T;
   double* Pq = a.Pq + (long)b * N * 36;
   double* Pd = a.Pd + (long)b * T;
-  double* Jb = a.J + (long)b * (N - 1) * 216;
+  double* Jb = a.J + (long)b * (N - 1) * ADM_JC;
   double* Ib = a.I + (long)b * m;
   double* qs = a.qs + (long)b * T;
   double* ls = a.ls + (long)b * m;
@@ -249,7 +282,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   double* E = a.E + (long)b * m;
   double* Dt = a.Dt + (long)b * T;
   double* Et = a.Et + (long)b * m;
-  double* Linv = a.Linv + (long)b * N * 324;
+  double* Linv = a.Linv + (long)b * N * ADM_LP;
   double* Cb = a.C + (long)b * (N - 1) * 216;
   double* wv = a.w + (long)b * T;
   double* xt = a.xt + (long)b * T;
@@ -331,9 +364,13 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
     }
     if (k < N - 1) {
       const double* L = LIN + LIN_STRIDE * k;
-      for (int e = l; e < 216; e += 64) {
-        const int i = e / 18, j = e - 18 * i;
-        Jb[216 * k + e] = E[12 * (k + 1) + i] * adm_jk(L, dt, i, j) * D[18 * k + j];
+      double* Jc = Jb + ADM_JC * k;
+      for (int e = l; e < ADM_JC; e += 64) {
+        int i, j;
+        if (e < 6) { i = e; j = e; }
+        else if (e < 12) { i = e - 6; j = e; }
+        else { i = 6 + (e - 12) / 18; j = (e - 12) % 18; }
+        Jc[e] = E[12 * (k + 1) + i] * adm_jk(L, dt, i, j) * D[18 * k + j];
       }
     }
   }
@@ -368,10 +405,10 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
     if (l < 12) sT0[l] = rv * (z[l] - ri * y[l]);
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
-      adm_stage(sL, Linv + 324 * k, 324, l);
+      adm_stage_L(sL, Linv + ADM_LP * k, l);
       if (k > 0) adm_stage(sC, Cb + 216 * (k - 1), 216, l);
       if (k < N - 1) {
-        adm_stage(sJ, Jb + 216 * k, 216, l);
+        adm_stage_J(sJ, Jb + ADM_JC * k, l);
         if (l < 12) {
           const int r = 12 * (k + 1) + l;
           sT1[l] = rv * (z[r] - ri * y[r]);
@@ -407,10 +444,10 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
     // relaxation and projection of block k+1 (block 0 at the end)
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
-      adm_stage(sL, Linv + 324 * k, 324, l);
+      adm_stage_L(sL, Linv + ADM_LP * k, l);
       if (k < N - 1) {
         adm_stage(sC, Cb + 216 * k, 216, l);
-        adm_stage(sJ, Jb + 216 * k, 216, l);
+        adm_stage_J(sJ, Jb + ADM_JC * k, l);
       }
       wave_sync();
       if (l < nk) {
@@ -427,8 +464,10 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       if (l < nk) {
         for (int i = l; i < nk; ++i) xk += sL[18 * i + l] * sR[i];
       }
-      // sW holds xt_{k+1}'s x part until block k+1's rows are done
-      if (l < nk) sR[l] = xk;  // (reuse: xt_k)
+      // sW holds xt_{k+1}'s x part until block k+1's rows are done; sR takes xt_k once every lane
+      // has read the right-hand side
+      wave_sync();
+      if (l < nk) sR[l] = xk;
       wave_sync();
       if (k < N - 1 && l < 12) {
         const int r = 12 * (k + 1) + l;

@@ -138,6 +138,7 @@ struct i7m_handle {
   // host-to-host i7m_solve split into chunks on two streams, so the copies of one chunk overlap
   // the solve of another (0 = one piece on h->stream; I7M_H2H_CHUNKS or cfg.h2h_chunks)
   int h2h_chunks = 0;
+  int admm_chunk = 0;  // I7M_ADMM_CHUNK: k_admm launched over this many problems at a time (0: all)
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   hipStream_t cs[2] = {nullptr, nullptr};
   hipStream_t cs2 = nullptr;  // h2h_pipe >= 2: the second solve stream (created on first use)
@@ -264,8 +265,8 @@ constexpr int ADM_NBUF = 19;
 void admm_sizes(long N, long sz[ADM_NBUF]) {
   const long T = 18 * N - 6, m = 12 * N;
   const long v[ADM_NBUF] = {T, m, m, T, 1,                                  // x z y q rho (state)
-                            36 * N, T, 216 * (N - 1), m, T, m, T, m, T, m,  // Pq Pd J I qs ls D E Dt Et
-                            324 * N, 216 * (N - 1), T, T};                  // Linv C w xt
+                            36 * N, T, ADM_JC * (N - 1), m, T, m, T, m, T, m,  // Pq Pd J I qs ls D E Dt Et
+                            ADM_LP * N, 216 * (N - 1), T, T};                  // Linv C w xt
   for (int i = 0; i < ADM_NBUF; ++i) sz[i] = v[i];
 }
 // AdmmArgs pointers of problems [b0, ...) in the handle's ADMM allocation (array-of-buffers, each
@@ -517,9 +518,18 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
     a.active = active;
     a.sol = sol;
     a.sqp_iter = sqp_iter;
-    return timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
-      hipExtLaunchKernelGGL(k_admm, dim3(P.B), dim3(64), 0, s, ea, eb, 0, a);
-    });
+    // I7M_ADMM_CHUNK = c > 0: the batch as consecutive launches of c problems, so one launch's
+    // factors (the blocks every OSQP iteration re-reads) can stay in the 256 MB MALL
+    const int chunk = h->admm_chunk > 0 ? std::min(h->admm_chunk, P.B) : P.B;
+    for (int lo = 0; lo < P.B; lo += chunk) {
+      a.b0 = lo;
+      const int n = std::min(chunk, P.B - lo);
+      const int rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
+        hipExtLaunchKernelGGL(k_admm, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+      });
+      if (rc2) return rc2;
+    }
+    return I7M_OK;
   }
   if ((rc = launch_riccati(h, s, W, P, xu, xs, active, sol))) return rc;
   *out = sol;
@@ -1005,6 +1015,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_H2H_CHUNKS")) h->h2h_chunks = std::atoi(e);
   if (const char* e = std::getenv("I7M_H2H_PIPE")) h->h2h_pipe = std::min(std::max(std::atoi(e), 0), 3);
   if (const char* e = std::getenv("I7M_H2H_TAPER")) h->h2h_taper = std::atoi(e) != 0;
+  if (const char* e = std::getenv("I7M_ADMM_CHUNK")) h->admm_chunk = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
