@@ -74,6 +74,42 @@ __device__ __forceinline__ void adm_stage_L(double* sL, const double* Lp, int l)
     sL[e] = j <= i ? Lp[adm_tri(i, j)] : 0.0;
   }
 }
+// A sweep step's blocks as one index space of ADM_ST doubles: packed Linv (171) | C (216) |
+// compact J (120); element e of it goes to LDS position adm_pf_dst(e) of [Linv 18 x 18 | C 12 x 18 |
+// J 12 x 18] (-1: beyond the space)
+constexpr int ADM_ST = ADM_LP + 216 + ADM_JC;
+__device__ __forceinline__ int adm_pf_dst(int e) {
+  if (e < ADM_LP) {
+    int i = 0;
+    while ((i + 1) * (i + 2) / 2 <= e) ++i;
+    return 18 * i + (e - i * (i + 1) / 2);
+  }
+  if (e < ADM_LP + 216) return 324 + (e - ADM_LP);
+  if (e < ADM_ST) {
+    const int c = e - ADM_LP - 216;
+    if (c < 6) return 540 + 18 * c + c;
+    if (c < 12) return 540 + 18 * (c - 6) + c;
+    return 540 + 18 * (6 + (c - 12) / 18) + (c - 12) % 18;
+  }
+  return -1;
+}
+__device__ __forceinline__ void adm_pf_load(double pf[8], const double* Lp, const double* Cc, const double* Jc, int l) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int e = l + 64 * t;
+    double v = 0.0;
+    if (e < ADM_LP) v = Lp[e];
+    else if (e < ADM_LP + 216) v = Cc ? Cc[e - ADM_LP] : 0.0;
+    else if (e < ADM_ST) v = Jc ? Jc[e - ADM_LP - 216] : 0.0;
+    pf[t] = v;
+  }
+}
+__device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, const int pdst[8]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (pdst[t] >= 0) sB[pdst[t]] = pf[t];
+}
+
 // entry (i, j) of the compact J_k in HBM
 __device__ __forceinline__ double adm_jc(const double* Jc, int i, int j) {
   if (i < 6) return j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
@@ -263,7 +299,10 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
-  __shared__ double sL[324], sC[216], sJ[216], sS[324], sCp[216], sR[32], sW[32], sT0[16], sT1[16];
+  __shared__ double sB[324 + 216 + 216], sS[324], sCp[216], sR[32], sW[32], sT0[16], sT1[16];
+  double* sL = sB;
+  double* sC = sB + 324;
+  double* sJ = sB + 540;
   const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
   const double* CO = a.cost + (long)b * N * COST_STRIDE;
   const double* QD = a.qpd + (long)b * (N - 1) * QPD_STRIDE;
@@ -398,29 +437,44 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   const double al = a.A.alpha, sg = a.A.sigma;
 
   // ---- 3. OSQP iterations
+  // Each sweep step stages the stage's blocks (packed Linv_k | C | compact J_k: ADM_ST doubles)
+  // through LDS; the next step's blocks are loaded into registers (8 per lane) while this step
+  // computes, after this step's own vector loads, so their latency hides behind the step.
+  // The LDS slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set by the factor.
+  int pdst[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) pdst[t] = adm_pf_dst(l + 64 * t);
   int it;
   bool solved = false;
   for (it = 1; it <= a.A.max_iter; ++it) {
     // forward sweep: w_k = Linv_k (rhs_k - C_{k-1} w_{k-1})
     if (l < 12) sT0[l] = rv * (z[l] - ri * y[l]);
+    double pf[8];
+    adm_pf_load(pf, Linv, nullptr, N > 1 ? Jb : nullptr, l);
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
-      adm_stage_L(sL, Linv + ADM_LP * k, l);
-      if (k > 0) adm_stage(sC, Cb + 216 * (k - 1), 216, l);
-      if (k < N - 1) {
-        adm_stage_J(sJ, Jb + ADM_JC * k, l);
-        if (l < 12) {
-          const int r = 12 * (k + 1) + l;
-          sT1[l] = rv * (z[r] - ri * y[r]);
-        }
+      wave_sync();
+      adm_pf_store(pf, sB, pdst);
+      // this step's vectors first, then the next step's blocks
+      double xe = 0.0, qe = 0.0, ie = 0.0, t1 = 0.0;
+      if (l < nk) {
+        xe = x[18 * k + l];
+        qe = qs[18 * k + l];
+        if (l < 12) ie = Ib[12 * k + l];
       }
+      if (k < N - 1 && l < 12) {
+        const int r = 12 * (k + 1) + l;
+        t1 = rv * (z[r] - ri * y[r]);
+      }
+      if (k + 1 < N) adm_pf_load(pf, Linv + ADM_LP * (k + 1), Cb + 216 * k, k + 1 < N - 1 ? Jb + ADM_JC * (k + 1) : nullptr, l);
+      if (k < N - 1 && l < 12) sT1[l] = t1;
       wave_sync();
       if (l < nk) {
-        const int j = l, e = 18 * k + j;
-        double acc = j < 12 ? Ib[12 * k + j] * sT0[j] : 0.0;
+        const int j = l;
+        double acc = j < 12 ? ie * sT0[j] : 0.0;
         if (k < N - 1)
           for (int i = 0; i < 12; ++i) acc += sJ[18 * i + j] * sT1[i];
-        double r = (sg * x[e] - qs[e]) + acc;
+        double r = (sg * xe - qe) + acc;
         if (k > 0 && j < 12) {
           double cw = 0.0;
           for (int q = 0; q < 18; ++q) cw += sC[18 * j + q] * sW[q];
@@ -437,21 +491,36 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       wave_sync();
       if (l < nk) sW[l] = wk;
       if (l < 12) sT0[l] = sT1[l];
-      wave_sync();
     }
     wave_sync_all();
     // backward sweep: xt_k = Linv_k' (w_k - C_k' xt_{k+1}); then A xt for the rows of block k+1,
-    // relaxation and projection of block k+1 (block 0 at the end)
+    // relaxation and projection of block k+1 (block 0 at the end).  Every global value a lane
+    // reads here it wrote itself (lane = index within the knot / block), so only LDS needs ordering.
+    adm_pf_load(pf, Linv + ADM_LP * (N - 1), nullptr, nullptr, l);
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
-      adm_stage_L(sL, Linv + ADM_LP * k, l);
+      wave_sync();
+      adm_pf_store(pf, sB, pdst);
+      double we = 0.0, zr0 = 0.0, yr0 = 0.0, lr0 = 0.0, ir0 = 0.0, xe1 = 0.0, xt1 = 0.0;
+      if (l < nk) we = wv[18 * k + l];
       if (k < N - 1) {
-        adm_stage(sC, Cb + 216 * k, 216, l);
-        adm_stage_J(sJ, Jb + ADM_JC * k, l);
+        if (l < 12) {
+          const int r = 12 * (k + 1) + l;
+          zr0 = z[r];
+          yr0 = y[r];
+          lr0 = ls[r];
+          ir0 = Ib[r];
+        }
+        const int nn = k + 1 < N - 1 ? 18 : 12;
+        if (l < nn) {
+          xe1 = x[18 * (k + 1) + l];
+          xt1 = xt[18 * (k + 1) + l];
+        }
       }
+      if (k > 0) adm_pf_load(pf, Linv + ADM_LP * (k - 1), Cb + 216 * (k - 1), Jb + ADM_JC * (k - 1), l);
       wave_sync();
       if (l < nk) {
-        double r = wv[18 * k + l];
+        double r = we;
         if (k < N - 1) {
           double acc = 0.0;
           for (int q = 0; q < 12; ++q) acc += sC[18 * q + l] * sW[q];
@@ -473,25 +542,22 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
         const int r = 12 * (k + 1) + l;
         double acc = 0.0;
         for (int j = 0; j < 18; ++j) acc += sJ[18 * l + j] * sR[j];
-        const double zt = acc + Ib[r] * sW[l];
-        const double zr = al * zt + (1.0 - al) * z[r];
-        double zn = zr + ri * y[r];
-        zn = fmin(fmax(zn, ls[r]), ls[r]);
-        y[r] = y[r] + rv * (zr - zn);
+        const double zt = acc + ir0 * sW[l];
+        const double zr = al * zt + (1.0 - al) * zr0;
+        double zn = zr + ri * yr0;
+        zn = fmin(fmax(zn, lr0), lr0);
+        y[r] = yr0 + rv * (zr - zn);
         z[r] = zn;
       }
       if (k < N - 1) {
         const int nn = k + 1 < N - 1 ? 18 : 12;
-        if (l < nn) {
-          const int e = 18 * (k + 1) + l;
-          x[e] = al * xt[e] + (1.0 - al) * x[e];
-        }
+        if (l < nn) x[18 * (k + 1) + l] = al * xt1 + (1.0 - al) * xe1;
       }
       if (l < nk) xt[18 * k + l] = xk;
-      wave_sync_all();
-      if (l < 12) sW[l] = sR[l];
       wave_sync();
+      if (l < 12) sW[l] = sR[l];
     }
+    wave_sync_all();
     // block 0 rows and x_0
     if (l < 12) {
       const double zt = Ib[l] * sW[l];
