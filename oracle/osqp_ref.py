@@ -45,7 +45,7 @@ class OSQPSolverRef:
 
     def __init__(self, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
                  qp="exact", P=None, box_mask=7, box_tol=1e-8, box_max_iters=30, fext6=None, fext_frame="local",
-                 osqp_settings=None):
+                 osqp_settings=None, osqp_box=0):
         self.P_ = P or rbd.params()
         # external wrench on joint 6 in every dynamics evaluation (batch_sqp's
         # set_external_wrench_batch; frame "world": converted per configuration, rbd.fext_list)
@@ -75,10 +75,33 @@ class OSQPSolverRef:
         self.B_k = np.zeros((self.nx, self.nq))
         self.cx_k = np.zeros(self.nx)
         if qp == "osqp":
-            # src/osqp_solver.py:38-40: one OSQP workspace, set up on the templates
+            # src/osqp_solver.py:38-40: one OSQP workspace, set up on the templates.  osqp_box
+            # (config 4 in ADMM mode, no reference counterpart): box rows l_b <= x_b <= u_b appended
+            # to A for the bounded entries of box_ipm.box_bounds(mask = osqp_box), values 1
             from .osqp_admm import OSQP
             self.osqp = OSQP()
-            self.osqp.setup(P=self.P, q=self.g, A=self.A, l=self.l, u=self.l, **(osqp_settings or {}))
+            A, l, u = self.A, self.l, self.l
+            self.osqp_box = osqp_box
+            if osqp_box:
+                from scipy.sparse import vstack, identity
+                from . import box_ipm
+                lo, hi, bm = box_ipm.box_bounds(self.P_, N, osqp_box)
+                self._bidx = np.flatnonzero(bm)
+                self._blo, self._bhi = lo[bm], hi[bm]
+                # where A's values and the box rows' land in the stacked matrix's CSC value order
+                At = A.copy()
+                At.data = np.arange(1, At.nnz + 1, dtype=float)
+                Ib = identity(self.traj_len, format="csc")[self._bidx]
+                Ib.data = -np.arange(1, Ib.nnz + 1, dtype=float)
+                code = vstack([At, Ib], format="csc")
+                code.sort_indices()
+                self._pos_a = np.flatnonzero(code.data > 0)[np.argsort(code.data[code.data > 0])]
+                self._pos_b = np.flatnonzero(code.data < 0)
+                self._nnz_full = code.nnz
+                A = vstack([A, identity(self.traj_len, format="csc")[self._bidx]], format="csc")
+                l = np.concatenate([self.l, self._blo])
+                u = np.concatenate([self.l, self._bhi])
+            self.osqp.setup(P=self.P, q=self.g, A=A, l=l, u=u, **(osqp_settings or {}))
 
     # src/osqp_solver.py:48-52
     def initialize_P(self):
@@ -212,8 +235,15 @@ class OSQPSolverRef:
         if self.qp == "osqp":
             # src/osqp_solver.py:140-143
             self.osqp.update(Px=self.Pdata)
-            self.osqp.update(Ax=self.Adata)
-            self.osqp.update(q=self.g, l=self.l, u=self.l)
+            if self.osqp_box:
+                ax = np.empty(self._nnz_full)
+                ax[self._pos_a] = self.Adata
+                ax[self._pos_b] = 1.0
+                self.osqp.update(Ax=ax)
+                self.osqp.update(q=self.g, l=np.concatenate([self.l, self._blo]), u=np.concatenate([self.l, self._bhi]))
+            else:
+                self.osqp.update(Ax=self.Adata)
+                self.osqp.update(q=self.g, l=self.l, u=self.l)
             x, y = self.osqp.solve()
             return QPResult(x, y, self.osqp.info["iter"])
         if self.qp == "admm":
