@@ -341,6 +341,8 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
                            "factor_stream": {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,
                                              "achieved_GBs": stream_gbs, "frac": stream_gbs / HBM_PEAK_GBS,
                                              "note": "the blocks every OSQP iteration re-reads (bench.admm_bytes_per_iter)"}}
+    # the reference's use: a closed loop whose every QP warm-starts from the instance's last one
+    res["closed_loop"] = mpc_closed_loop(model, stream, local, B, N, steps=10, qp_mode=_lib.QP_ADMM)
     if native is not None:
         from oracle import cpu
         lib_path, build_desc = native
@@ -416,20 +418,23 @@ def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: 
             "finite": bool(np.isfinite(out).all())}
 
 
-def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps: int = 20):
+def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps: int = 20, qp_mode=None):
     """The batched closed loop (MPC_OSQP.run_mpc for B instances, i7m_mpc_run: goal update, SQP,
     rk4 plant, shift and pins per MPC step, all on the device; src/osqp_mpc.py:14-72 and the batch
     axis of src/gato_mpc_batch.py:76-217): instance-steps per second over `steps` MPC steps of the
     config-3 draws, one synchronous call (with its H2D of the start states and D2H of the
-    histories), after one warm-up call."""
+    histories), after one warm-up call.  qp_mode _lib.QP_ADMM: every QP by OSQP's iteration, warm
+    started from the instance's previous QP as the reference's loop runs."""
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.synthetic import draw_states
 
-    h = _lib.Handle(model, N=N, max_batch=B, device_id=local)
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=_lib.QP_DIRECT if qp_mode is None else qp_mode)
     h.set_stream(stream.cuda_stream)
     xs, qg = draw_states(model, B, seed=42 + 3)
     ends = np.vstack([h.eepos(qg[:1]), h.eepos(qg[1:2])])
     h.mpc_run(xs, ends, 2)
+    if qp_mode == _lib.QP_ADMM:
+        h.admm_reset()
     t0 = time.perf_counter()
     d, q, _, _ = h.mpc_run(xs, ends, steps)
     el = time.perf_counter() - t0
