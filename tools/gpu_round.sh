@@ -35,6 +35,13 @@ if has pmc; then
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d $O/pmc_sq -o sq -- python $R/tools/profile_kernels.py --steps 2 > $O/pmc_sq.log 2>&1 || { tail -20 $O/pmc_sq.log; exit 6; }
   python $R/tools/sq_summary.py $O/pmc_sq/sq_counter_collection.csv > $O/sq_summary.json
 fi
+if has admm; then
+  # config 3 in ADMM mode (B = 4096, N = 32, cold OSQP state per solve): trace + FETCH / WRITE of k_admm
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/admm_trace -o run -- python $R/tools/profile_kernels.py --admm --steps 2 --warmup 1 > $O/admm_trace.log 2>&1 || { tail -20 $O/admm_trace.log; exit 14; }
+  python $R/tools/trace_summary.py $O/admm_trace/run_kernel_trace.csv --batch 4096 --N 32 > $O/admm_trace_summary.json
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/admm_fetch -o fetch -- python $R/tools/profile_kernels.py --admm --steps 1 --warmup 1 > $O/admm_fetch.log 2>&1 || { tail -20 $O/admm_fetch.log; exit 15; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/admm_write -o write -- python $R/tools/profile_kernels.py --admm --steps 1 --warmup 1 > $O/admm_write.log 2>&1 || { tail -20 $O/admm_write.log; exit 16; }
+fi
 if has c4; then
   # config 4 (B = 4096, N = 64, box rows): trace + FETCH / WRITE of k_ipm_fused
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4_trace -o run -- python $R/tools/profile_kernels.py --box --N 64 --steps 2 --warmup 1 > $O/c4_trace.log 2>&1 || { tail -20 $O/c4_trace.log; exit 7; }

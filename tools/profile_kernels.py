@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--box", action="store_true", help="config 4: box rows (I7M_QP_BOX), seed 46")
+    ap.add_argument("--admm", action="store_true", help="config 3 in ADMM mode (I7M_QP_ADMM), cold OSQP state per solve")
     ap.add_argument("--pipeline", default="split", choices=["split", "fused", "fused_iter"])
     a = ap.parse_args()
     import torch
@@ -29,7 +30,8 @@ def main():
     dev = torch.device("cuda", 0)
     model = default_model()
     pipe = {"split": _lib.PIPE_SPLIT, "fused": _lib.PIPE_FUSED, "fused_iter": _lib.PIPE_FUSED_ITER}[a.pipeline]
-    h = _lib.Handle(model, N=a.N, max_batch=a.batch, pipeline=pipe, **({"qp_mode": _lib.QP_BOX} if a.box else {}))
+    mode = {"qp_mode": _lib.QP_BOX} if a.box else ({"qp_mode": _lib.QP_ADMM} if a.admm else {})
+    h = _lib.Handle(model, N=a.N, max_batch=a.batch, pipeline=pipe, **mode)
     s = torch.cuda.Stream(dev)
     torch.cuda.set_stream(s)
     h.set_stream(s.cuda_stream)
@@ -37,6 +39,8 @@ def main():
     t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
     t_out = torch.empty_like(t_xu)
     for _ in range(a.warmup + a.steps):
+        if a.admm:
+            h.admm_reset()
         h.solve_device(a.batch, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
     torch.cuda.synchronize(dev)
     print("profiled", a.warmup + a.steps, "solves of B", a.batch, "N", a.N)
