@@ -438,36 +438,49 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
 
   // ---- 3. OSQP iterations
   // Each sweep step stages the stage's blocks (packed Linv_k | C | compact J_k: ADM_ST doubles)
-  // through LDS; the next step's blocks are loaded into registers (8 per lane) while this step
-  // computes, after this step's own vector loads, so their latency hides behind the step.
-  // The LDS slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set by the factor.
+  // through LDS.  Everything the next step reads from HBM — its blocks (8 doubles per lane) and
+  // its vector entries (x, q, the -I entries, z, y, l of the rows it finishes) — is loaded into
+  // registers at the start of this step, before this step's stores, so the loads' latency hides
+  // behind the step and waiting for them never waits for a store (vmcnt is in order).  The LDS
+  // slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set by the factor.
   int pdst[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) pdst[t] = adm_pf_dst(l + 64 * t);
   int it;
   bool solved = false;
+  const bool lx = l < 18, lr = l < 12;
   for (it = 1; it <= a.A.max_iter; ++it) {
     // forward sweep: w_k = Linv_k (rhs_k - C_{k-1} w_{k-1})
-    if (l < 12) sT0[l] = rv * (z[l] - ri * y[l]);
-    double pf[8];
+    double pf[8], fx = 0.0, fq = 0.0, fi = 0.0, fz = 0.0, fy = 0.0;
     adm_pf_load(pf, Linv, nullptr, N > 1 ? Jb : nullptr, l);
+    if (lx) { fx = x[l]; fq = qs[l]; }
+    if (lr) {
+      fi = Ib[l];
+      fz = z[12 + l];
+      fy = y[12 + l];
+      sT0[l] = rv * (z[l] - ri * y[l]);
+    }
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
       wave_sync();
       adm_pf_store(pf, sB, pdst);
-      // this step's vectors first, then the next step's blocks
-      double xe = 0.0, qe = 0.0, ie = 0.0, t1 = 0.0;
-      if (l < nk) {
-        xe = x[18 * k + l];
-        qe = qs[18 * k + l];
-        if (l < 12) ie = Ib[12 * k + l];
+      const double xe = fx, qe = fq, ie = fi, t1 = rv * (fz - ri * fy);
+      if (k + 1 < N) {
+        adm_pf_load(pf, Linv + ADM_LP * (k + 1), Cb + 216 * k, k + 1 < N - 1 ? Jb + ADM_JC * (k + 1) : nullptr, l);
+        const int n1 = k + 1 < N - 1 ? 18 : 12;
+        if (l < n1) {
+          fx = x[18 * (k + 1) + l];
+          fq = qs[18 * (k + 1) + l];
+        }
+        if (lr) {
+          fi = Ib[12 * (k + 1) + l];
+          if (k + 2 < N) {
+            fz = z[12 * (k + 2) + l];
+            fy = y[12 * (k + 2) + l];
+          }
+        }
       }
-      if (k < N - 1 && l < 12) {
-        const int r = 12 * (k + 1) + l;
-        t1 = rv * (z[r] - ri * y[r]);
-      }
-      if (k + 1 < N) adm_pf_load(pf, Linv + ADM_LP * (k + 1), Cb + 216 * k, k + 1 < N - 1 ? Jb + ADM_JC * (k + 1) : nullptr, l);
-      if (k < N - 1 && l < 12) sT1[l] = t1;
+      if (k < N - 1 && lr) sT1[l] = t1;
       wave_sync();
       if (l < nk) {
         const int j = l;
@@ -490,34 +503,32 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       }
       wave_sync();
       if (l < nk) sW[l] = wk;
-      if (l < 12) sT0[l] = sT1[l];
+      if (lr) sT0[l] = sT1[l];
     }
-    wave_sync_all();
     // backward sweep: xt_k = Linv_k' (w_k - C_k' xt_{k+1}); then A xt for the rows of block k+1,
-    // relaxation and projection of block k+1 (block 0 at the end).  Every global value a lane
-    // reads here it wrote itself (lane = index within the knot / block), so only LDS needs ordering.
+    // the relaxation of x_{k+1}, and the projection and dual update of block k+1 (block 0 after
+    // the sweep).  xt never leaves registers: step k needs only xt_k and xt_{k+1}.  Every global
+    // value a lane reads it wrote itself (lane = index within the knot / block).
+    double bw = 0.0, bz = 0.0, by = 0.0, bl = 0.0, bi = 0.0, bx = 0.0, xtp = 0.0;
     adm_pf_load(pf, Linv + ADM_LP * (N - 1), nullptr, nullptr, l);
+    if (l < 12) bw = wv[18 * (N - 1) + l];
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
       wave_sync();
       adm_pf_store(pf, sB, pdst);
-      double we = 0.0, zr0 = 0.0, yr0 = 0.0, lr0 = 0.0, ir0 = 0.0, xe1 = 0.0, xt1 = 0.0;
-      if (l < nk) we = wv[18 * k + l];
-      if (k < N - 1) {
-        if (l < 12) {
-          const int r = 12 * (k + 1) + l;
-          zr0 = z[r];
-          yr0 = y[r];
-          lr0 = ls[r];
-          ir0 = Ib[r];
-        }
-        const int nn = k + 1 < N - 1 ? 18 : 12;
-        if (l < nn) {
-          xe1 = x[18 * (k + 1) + l];
-          xt1 = xt[18 * (k + 1) + l];
-        }
+      const double we = bw, zr0 = bz, yr0 = by, lr0 = bl, ir0 = bi, xe1 = bx;
+      // step k - 1's loads: its blocks, w_{k-1}, block k's rows, x_k (block 0's rows and x_0 at k = 0)
+      if (k > 0) {
+        adm_pf_load(pf, Linv + ADM_LP * (k - 1), Cb + 216 * (k - 1), Jb + ADM_JC * (k - 1), l);
+        if (lx) bw = wv[18 * (k - 1) + l];
       }
-      if (k > 0) adm_pf_load(pf, Linv + ADM_LP * (k - 1), Cb + 216 * (k - 1), Jb + ADM_JC * (k - 1), l);
+      if (lr) {
+        bz = z[12 * k + l];
+        by = y[12 * k + l];
+        bl = ls[12 * k + l];
+        bi = Ib[12 * k + l];
+      }
+      if (l < nk) bx = x[18 * k + l];
       wave_sync();
       if (l < nk) {
         double r = we;
@@ -538,7 +549,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       wave_sync();
       if (l < nk) sR[l] = xk;
       wave_sync();
-      if (k < N - 1 && l < 12) {
+      if (k < N - 1 && lr) {
         const int r = 12 * (k + 1) + l;
         double acc = 0.0;
         for (int j = 0; j < 18; ++j) acc += sJ[18 * l + j] * sR[j];
@@ -551,23 +562,22 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       }
       if (k < N - 1) {
         const int nn = k + 1 < N - 1 ? 18 : 12;
-        if (l < nn) x[18 * (k + 1) + l] = al * xt1 + (1.0 - al) * xe1;
+        if (l < nn) x[18 * (k + 1) + l] = al * xtp + (1.0 - al) * xe1;
       }
-      if (l < nk) xt[18 * k + l] = xk;
+      xtp = xk;
       wave_sync();
-      if (l < 12) sW[l] = sR[l];
+      if (lr) sW[l] = sR[l];
     }
-    wave_sync_all();
-    // block 0 rows and x_0
-    if (l < 12) {
-      const double zt = Ib[l] * sW[l];
-      const double zr = al * zt + (1.0 - al) * z[l];
-      double zn = zr + ri * y[l];
-      zn = fmin(fmax(zn, ls[l]), ls[l]);
-      y[l] = y[l] + rv * (zr - zn);
+    // block 0 rows and x_0 (their old values were loaded at k = 0)
+    if (lr) {
+      const double zt = bi * sW[l];
+      const double zr = al * zt + (1.0 - al) * bz;
+      double zn = zr + ri * by;
+      zn = fmin(fmax(zn, bl), bl);
+      y[l] = by + rv * (zr - zn);
       z[l] = zn;
     }
-    if (l < 18) x[l] = al * xt[l] + (1.0 - al) * x[l];
+    if (lx) x[l] = al * xtp + (1.0 - al) * bx;
     wave_sync_all();
     const bool chk = a.A.check && it % a.A.check == 0;
     const bool adapt = a.A.adapt_interval && it % a.A.adapt_interval == 0;

@@ -144,7 +144,11 @@ def test_config4_every_problem_matches_cpu_port(lib, model, N, B, seed):
     for k in range(2):
         sel = st["n_alphas"] > k
         np.testing.assert_array_equal(st["alphas"][sel, k], al[sel, k])
-    np.testing.assert_array_equal(it, rit[np.arange(B), qp - 1])
+    rlast = rit[np.arange(B), qp - 1]
+    bad = np.flatnonzero(it != rlast)
+    assert bad.size == 0, (f"{bad.size} of {B} differ: problems {bad[:12].tolist()}, GPU {it[bad[:12]].tolist()}, port "
+                           f"{rlast[bad[:12]].tolist()}, port per SQP iteration {rit[bad[:4]].tolist()}, qp_iters "
+                           f"{qp[bad[:12]].tolist()}, GPU conv {conv[bad[:12]].tolist()}, port conv {rconv[bad[:12]].tolist()}")
     np.testing.assert_array_equal(conv, rconv)
     assert conv.all(), conv.mean()
     rel = np.linalg.norm(out - ref, axis=1) / np.linalg.norm(ref, axis=1)
