@@ -110,6 +110,24 @@ __device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, con
     if (pdst[t] >= 0) sB[pdst[t]] = pf[t];
 }
 
+// init + sum_i a[sa i] b[i] over n LDS operands, summed in i order: every operand read is issued
+// before the fma chain, so the chain pays one LDS latency instead of one per term (the dot
+// products of the sweeps run over fixed lengths; Linv's upper triangle and the padding of the
+// last knot's 12 x 12 blocks are exact zeros, which add nothing)
+template <int n>
+__device__ __forceinline__ double adm_dot(double init, const double* a, int sa, const double* b) {
+  double av[n], bv[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    av[i] = a[sa * i];
+    bv[i] = b[i];
+  }
+  double acc = init;
+#pragma unroll
+  for (int i = 0; i < n; ++i) acc += av[i] * bv[i];
+  return acc;
+}
+
 // entry (i, j) of the compact J_k in HBM
 __device__ __forceinline__ double adm_jc(const double* Jc, int i, int j) {
   if (i < 6) return j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
@@ -485,20 +503,15 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       if (l < nk) {
         const int j = l;
         double acc = j < 12 ? ie * sT0[j] : 0.0;
-        if (k < N - 1)
-          for (int i = 0; i < 12; ++i) acc += sJ[18 * i + j] * sT1[i];
+        if (k < N - 1) acc = adm_dot<12>(acc, sJ + j, 18, sT1);
         double r = (sg * xe - qe) + acc;
-        if (k > 0 && j < 12) {
-          double cw = 0.0;
-          for (int q = 0; q < 18; ++q) cw += sC[18 * j + q] * sW[q];
-          r -= cw;
-        }
+        if (k > 0 && j < 12) r -= adm_dot<18>(0.0, sC + 18 * j, 1, sW);
         sR[j] = r;
       }
       wave_sync();
       double wk = 0.0;
       if (l < nk) {
-        for (int j = 0; j <= l; ++j) wk += sL[18 * l + j] * sR[j];
+        wk = adm_dot<18>(0.0, sL + 18 * l, 1, sR);
         wv[18 * k + l] = wk;
       }
       wave_sync();
@@ -532,18 +545,12 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       wave_sync();
       if (l < nk) {
         double r = we;
-        if (k < N - 1) {
-          double acc = 0.0;
-          for (int q = 0; q < 12; ++q) acc += sC[18 * q + l] * sW[q];
-          r -= acc;
-        }
+        if (k < N - 1) r -= adm_dot<12>(0.0, sC + l, 18, sW);
         sR[l] = r;
       }
       wave_sync();
       double xk = 0.0;
-      if (l < nk) {
-        for (int i = l; i < nk; ++i) xk += sL[18 * i + l] * sR[i];
-      }
+      if (l < nk) xk = adm_dot<18>(0.0, sL + l, 18, sR);
       // sW holds xt_{k+1}'s x part until block k+1's rows are done; sR takes xt_k once every lane
       // has read the right-hand side
       wave_sync();
@@ -551,9 +558,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
       wave_sync();
       if (k < N - 1 && lr) {
         const int r = 12 * (k + 1) + l;
-        double acc = 0.0;
-        for (int j = 0; j < 18; ++j) acc += sJ[18 * l + j] * sR[j];
-        const double zt = acc + ir0 * sW[l];
+        const double zt = adm_dot<18>(0.0, sJ + 18 * l, 1, sR) + ir0 * sW[l];
         const double zr = al * zt + (1.0 - al) * zr0;
         double zn = zr + ri * yr0;
         zn = fmin(fmax(zn, lr0), lr0);

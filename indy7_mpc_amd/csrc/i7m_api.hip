@@ -629,8 +629,9 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
     if (rc) return rc;
     const double* qsol = nullptr;
     if ((rc = solve_qp(h, s, W, P, xin, d_xs, act, qbuf, &qsol, it))) return rc;
-    if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, act, d_st, nullptr, it, 0,
-                                h->ablate != 6)))
+    // mode 2: the ADMM mode's QP solver carries state, so an alpha = 0 iteration is re-solved
+    if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, act, d_st, nullptr, it,
+                                h->cfg.qp_mode == I7M_QP_ADMM ? 2 : 0, h->ablate != 6)))
       return rc;
   }
   return I7M_OK;

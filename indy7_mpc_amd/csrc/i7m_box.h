@@ -374,6 +374,10 @@ __global__ void __launch_bounds__(64) k_ipm_init(const DevModel* __restrict__ Mg
                                                  IpmState* __restrict__ st, int* __restrict__ ipm_active) {
   const int b = blockIdx.x;
   if (b >= P.B) return;
+  if (active && !active[b]) {  // a finished problem keeps its last QP's state and record
+    if (threadIdx.x == 0) ipm_active[b] = 0;
+    return;
+  }
   __shared__ BoxTab Bt;
   box_tab_fill(*Mg, BP.mask, &Bt);
   const IpmState S = ipm_init_body(Bt, P, BP, b, xeq, x, zl, zu, sig, h);
@@ -457,6 +461,7 @@ k_ipm_fused(IpmFusedArgs args) {
   I7M_TL(4);
   const int b = blockIdx.x;
   if (b >= args.P.B) return;
+  if (args.active && !args.active[b]) return;  // a finished problem keeps its last QP's state and record
   __shared__ double sh[MO_TOTAL];
   __shared__ BoxTab Bt;
   IpmState S;

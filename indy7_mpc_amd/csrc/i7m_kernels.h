@@ -112,7 +112,10 @@ __device__ __forceinline__ void merit_knot(const DevModel& Md, const SolveParams
 // Line search (+ step) — one wavefront per problem.  Candidates: 0 = base point (merit of XU
 // itself, src/osqp_sqp.py:52-55), 1..8 = alphas 1, 1/2, ..., 1/128.  R = max(1, 64/N)
 // candidates per round; the first accepted candidate in alpha order wins (identical to the
-// sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha.
+// sequential loop).  mode 0: apply step + stats + break flag; mode 1: only output alpha; mode 2: as
+// 0 for a QP solver that carries state between calls (I7M_QP_ADMM): alpha = 0 records this
+// iteration only, and the next iteration re-solves (src/osqp_sqp.py:81-82 `continue`; OSQP's
+// warm start makes the re-solve differ).
 // With lin / cost (the k_linearize outputs at this XU) the base merit is assembled from them —
 // a = ABA(q, v, u) and |e| of every knot are already there — so no round evaluates candidate 0.
 // SPEC: Indy7 constants baked in (kIndy7Model, generated from the URDF) instead of read from Mg.
@@ -491,11 +494,18 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   double* XOE = KA ? KE->xu_out + (long)b * PE.T : XO;
   if (alpha == 0.0) {
     // src/osqp_sqp.py:81-82: `continue` re-solves the SAME QP from the same XU; the exact
-    // solve is deterministic, so every remaining iteration repeats alpha = 0.
+    // solve is deterministic, so every remaining iteration repeats alpha = 0.  A stateful QP
+    // solver (mode 2) re-solves from its new state: this iteration only.
     if (l == 0) {
-      for (int it = iterE; it < PE.max_iters; ++it) st->alphas[st->n_alphas++] = 0.0;
-      st->qp_iters = PE.max_iters;
-      actE[b] = 0;
+      if (modeE == 2) {
+        st->alphas[st->n_alphas++] = 0.0;
+        st->qp_iters = iterE + 1;
+        if (iterE + 1 >= PE.max_iters) actE[b] = 0;
+      } else {
+        for (int it = iterE; it < PE.max_iters; ++it) st->alphas[st->n_alphas++] = 0.0;
+        st->qp_iters = PE.max_iters;
+        actE[b] = 0;
+      }
     }
     if (XOE != XE)
       for (int e = l; e < PE.T; e += 64) XOE[e] = sXD[e].x;

@@ -39,10 +39,12 @@ def _rel(a, b):
     return np.linalg.norm(a - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-300)
 
 
-@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43)])
+@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43), (16, 512, 41)])
 def test_admm_solves_match_port(lib, model, N, B, seed):
     """Two consecutive solves (the second warm-started from the first's OSQP state) on the GPU and
-    on the port: same OSQP iterations and steps, same XU and state."""
+    on the port: same OSQP iterations and steps, same XU and state.  (16, 512, 41) holds problems
+    whose first line search finds no step (alpha = 0): src/osqp_sqp.py:81-82 re-solves the same QP,
+    which OSQP's warm start makes a different iterate — the GPU re-solves too (k_linesearch mode 2)."""
     xcur, goals, XU = synthetic_batch(B, N, seed)
     h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
     st = cpu.AdmmState(B, N)
@@ -52,6 +54,8 @@ def test_admm_solves_match_port(lib, model, N, B, seed):
         it, rho = h.admm_stats(B)
         ref, qp, al, _, it_r = cpu.solve_admm(xcur, goals, xin, N, st)
         np.testing.assert_array_equal(s["qp_iters"], qp)
+        if (N, B, seed) == (16, 512, 41) and call == 0:
+            assert (al[:, 0] == 0.0).sum() >= 5  # the case this parameter set is for
         for b in range(B):
             n = qp[b]
             np.testing.assert_array_equal(it[b, :n], it_r[b, :n], err_msg=f"call {call} problem {b}")
