@@ -19,8 +19,8 @@
 //      [l, u], dual update; every `check` iterations the unscaled residuals and (OSQP 1.x) the
 //      duality gap; optional adaptive rho with a refactorisation.
 // Every row of A is an equality row (l = u), so rho_vec = 1e3 rho (RHO_EQ_OVER_RHO_INEQ).
-// Per-stage blocks live in HBM (Linv packed 171, C 216, scaled J compact 120 doubles) and are
-// staged through LDS per stage; the sweeps are bound by those reads.
+// Per-stage blocks live in HBM as one record per stage (Linv packed 171, C 216, scaled J compact
+// 120 doubles) and are staged through LDS per stage.
 #pragma once
 
 #include "i7m_kernels.h"
@@ -45,7 +45,7 @@ struct AdmmArgs {
   // OSQP state per problem (scaled x, z, y; the previous QP's q, unscaled; rho)
   double *sx, *sz, *sy, *sq, *srho;
   // scratch per problem
-  double *Pq, *Pd, *J, *I, *qs, *ls, *D, *E, *Dt, *Et, *Linv, *C, *w, *xt;
+  double *Pq, *Pd, *I, *qs, *ls, *D, *E, *Dt, *Et, *R, *w;
   int* iters;  // (B, I7M_MAX_SQP): OSQP iterations of SQP iteration `sqp_iter`
   int sqp_iter;
   int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
@@ -55,7 +55,16 @@ struct AdmmArgs {
 // factor packed lower-triangular (171 of 324), the scaled J_k as its q rows' two diagonals
 // (E_i D_i for I, E_i dt D_{6+i} for dt I) and its v rows (6 x 18): 120 of 216.  Staged to LDS
 // unpacked, so the arithmetic is the dense form's (the dropped entries are exact zeros).
+#ifndef I7M_ADMM_WPE
+#define I7M_ADMM_WPE 2  // waves per SIMD k_admm is compiled for (registers: <= 256 / wave at 2)
+#endif
 constexpr int ADM_LP = 171, ADM_JC = 120;
+// One record per stage, N + 1 per problem: record k = [Linv_k packed (171) | C_{k-1} (216; record
+// 0's unused) | compact J_k (120; record N-1's and N's unused)].  The forward sweep's step k reads
+// record k as it is; the backward sweep's step k needs C_k, which is record k+1's C — the same
+// element offsets plus one record for the C part.  So a step's blocks are one base pointer and
+// per-lane constant offsets (no per-element pointer selects).
+constexpr int ADM_REC = ADM_LP + 216 + ADM_JC, REC_C = ADM_LP, REC_J = ADM_LP + 216;
 __device__ __forceinline__ int adm_tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // dense 12 x 18 J_k into LDS from its compact form
 __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
@@ -93,21 +102,26 @@ __device__ __forceinline__ int adm_pf_dst(int e) {
   }
   return -1;
 }
-__device__ __forceinline__ void adm_pf_load(double pf[8], const double* Lp, const double* Cc, const double* Jc, int l) {
+// A lane's element t of a step: its record offset for the forward sweep (bits 0-9), for the
+// backward sweep (bits 10-19) and its LDS slot + 1 (bits 20-29; 0 = none), packed in one register.
+__device__ __forceinline__ int adm_pf_code(int e) {
+  if (e >= ADM_ST) return 0;
+  const int ob = e + (e >= REC_C && e < REC_J ? ADM_REC : 0);
+  return e | (ob << 10) | ((adm_pf_dst(e) + 1) << 20);
+}
+// one unconditional load per element from a record base and the lane's fixed offsets (lanes past
+// the space re-read the base): no branches around the loads, so the wait for them is a counted
+// vmcnt, not a vmcnt(0) at a control-flow join.  sh: 0 forward offsets, 10 backward.
+__device__ __forceinline__ void adm_pf_load(double pf[8], const double* rec, const int code[8], int sh) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) pf[t] = rec[(code[t] >> sh) & 1023];
+}
+__device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, const int code[8]) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const int e = l + 64 * t;
-    double v = 0.0;
-    if (e < ADM_LP) v = Lp[e];
-    else if (e < ADM_LP + 216) v = Cc ? Cc[e - ADM_LP] : 0.0;
-    else if (e < ADM_ST) v = Jc ? Jc[e - ADM_LP - 216] : 0.0;
-    pf[t] = v;
+    const int d = code[t] >> 20;
+    if (d) sB[d - 1] = pf[t];
   }
-}
-__device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, const int pdst[8]) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-    if (pdst[t] >= 0) sB[pdst[t]] = pf[t];
 }
 
 // init + sum_i a[sa i] b[i] over n LDS operands, summed in i order: every operand read is issued
@@ -174,7 +188,7 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     if (k == 0) {
       ax = Ib[r] * x[i];
     } else {
-      const double* G = Jb + ADM_JC * (k - 1);
+      const double* G = Jb + ADM_REC * (k - 1);
       const double* xk = x + 18 * (k - 1);
       double acc = 0.0;
       for (int j = 0; j < 18; ++j) acc += adm_jc(G, i, j) * xk[j];
@@ -200,7 +214,7 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     }
     double aty = j < 12 ? Ib[12 * k + j] * y[12 * k + j] : 0.0;
     if (k < N - 1) {
-      const double* G = Jb + ADM_JC * k;
+      const double* G = Jb + ADM_REC * k;
       for (int i = 0; i < 12; ++i) aty += adm_jc(G, i, j) * y[12 * (k + 1) + i];
     }
     const double di = 1.0 / D[e];
@@ -236,14 +250,14 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
 }
 
 // M = P + sigma I + A' rho A, block Cholesky with inverted diagonal factors (as Solver::
-// admm_factor of the port): Linv (N, 18 x 18) and C (N-1, 12 x 18) to HBM
+// admm_factor of the port): Linv_k (packed) into record k, C_k into record k+1
 __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
-                           const double* Jb, double* Linv, double* Cb, double* sS, double* sJ, double* sL, double* sCp,
+                           double* Rb, double* sS, double* sJ, double* sL, double* sCp,
                            int l) {
   const double re = 1e3 * rho, sigma = a.A.sigma;
   for (int k = 0; k < N; ++k) {
     const int nk = k < N - 1 ? 18 : 12;
-    if (k < N - 1) adm_stage_J(sJ, Jb + ADM_JC * k, l);
+    if (k < N - 1) adm_stage_J(sJ, Rb + ADM_REC * k + REC_J, l);
     wave_sync();
     for (int e = l; e < 324; e += 64) {
       const int i = e / 18, j = e - 18 * i;
@@ -296,7 +310,7 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
     wave_sync();
     for (int e = l; e < 324; e += 64) {
       const int i = e / 18, j = e - 18 * i;
-      if (j <= i) Linv[ADM_LP * k + adm_tri(i, j)] = sL[e];
+      if (j <= i) Rb[ADM_REC * k + adm_tri(i, j)] = sL[e];
     }
     if (k < N - 1) {
       for (int e = l; e < 216; e += 64) {
@@ -305,14 +319,14 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
         for (int q = 0; q <= j; ++q) acc += sJ[18 * i + q] * sL[18 * j + q];
         const double cv = re * Ib[12 * (k + 1) + i] * acc;
         sCp[e] = cv;
-        Cb[216 * k + e] = cv;
+        Rb[ADM_REC * (k + 1) + REC_C + e] = cv;
       }
     }
     wave_sync_all();
   }
 }
 
-__global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_WPE, I7M_ADMM_WPE))) k_admm(AdmmArgs a) {
   const int b = a.b0 + blockIdx.x;
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
@@ -331,7 +345,8 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   double* qold = a.sq + (long)b * T;
   double* Pq = a.Pq + (long)b * N * 36;
   double* Pd = a.Pd + (long)b * T;
-  double* Jb = a.J + (long)b * (N - 1) * ADM_JC;
+  double* Rb = a.R + (long)b * (N + 1) * ADM_REC;
+  double* Jb = Rb + REC_J;  // J_k at Jb + ADM_REC k
   double* Ib = a.I + (long)b * m;
   double* qs = a.qs + (long)b * T;
   double* ls = a.ls + (long)b * m;
@@ -339,10 +354,8 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   double* E = a.E + (long)b * m;
   double* Dt = a.Dt + (long)b * T;
   double* Et = a.Et + (long)b * m;
-  double* Linv = a.Linv + (long)b * N * ADM_LP;
-  double* Cb = a.C + (long)b * (N - 1) * 216;
+
   double* wv = a.w + (long)b * T;
-  double* xt = a.xt + (long)b * T;
   const double dt = P.dt;
 
   // ---- 1. unscaled P blocks (src/osqp_solver.py:103-135), the previous q, D = E = 1
@@ -421,7 +434,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
     }
     if (k < N - 1) {
       const double* L = LIN + LIN_STRIDE * k;
-      double* Jc = Jb + ADM_JC * k;
+      double* Jc = Jb + ADM_REC * k;
       for (int e = l; e < ADM_JC; e += 64) {
         int i, j;
         if (e < 6) { i = e; j = e; }
@@ -450,7 +463,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
 
   // ---- 2. factor
   double rho = a.srho[b];
-  adm_factor(a, N, rho, Pq, Pd, Ib, Jb, Linv, Cb, sS, sJ, sL, sCp, l);
+  adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
   double rv = 1e3 * rho, ri = 1.0 / rv;
   const double al = a.A.alpha, sg = a.A.sigma;
 
@@ -461,42 +474,39 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
   // registers at the start of this step, before this step's stores, so the loads' latency hides
   // behind the step and waiting for them never waits for a store (vmcnt is in order).  The LDS
   // slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set by the factor.
-  int pdst[8];
+  int pcode[8];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) pdst[t] = adm_pf_dst(l + 64 * t);
+  for (int t = 0; t < 8; ++t) pcode[t] = adm_pf_code(l + 64 * t);
   int it;
   bool solved = false;
   const bool lx = l < 18, lr = l < 12;
   for (it = 1; it <= a.A.max_iter; ++it) {
     // forward sweep: w_k = Linv_k (rhs_k - C_{k-1} w_{k-1})
-    double pf[8], fx = 0.0, fq = 0.0, fi = 0.0, fz = 0.0, fy = 0.0;
-    adm_pf_load(pf, Linv, nullptr, N > 1 ? Jb : nullptr, l);
-    if (lx) { fx = x[l]; fq = qs[l]; }
-    if (lr) {
-      fi = Ib[l];
-      fz = z[12 + l];
-      fy = y[12 + l];
-      sT0[l] = rv * (z[l] - ri * y[l]);
-    }
+    // (the next step's loads are unconditional, at clamped stage / lane indices: in bounds always,
+    // unused where a stage has no such block or entry)
+    const int l17 = l < 17 ? l : 17, l11 = l < 11 ? l : 11;
+    double pf[8], fx, fq, fi, fz, fy;
+    adm_pf_load(pf, Rb, pcode, 0);
+    fx = x[l17];
+    fq = qs[l17];
+    fi = Ib[l11];
+    fz = z[12 + l11];
+    fy = y[12 + l11];
+    if (lr) sT0[l] = rv * (z[l] - ri * y[l]);
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
       wave_sync();
-      adm_pf_store(pf, sB, pdst);
+      adm_pf_store(pf, sB, pcode);
       const double xe = fx, qe = fq, ie = fi, t1 = rv * (fz - ri * fy);
-      if (k + 1 < N) {
-        adm_pf_load(pf, Linv + ADM_LP * (k + 1), Cb + 216 * k, k + 1 < N - 1 ? Jb + ADM_JC * (k + 1) : nullptr, l);
-        const int n1 = k + 1 < N - 1 ? 18 : 12;
-        if (l < n1) {
-          fx = x[18 * (k + 1) + l];
-          fq = qs[18 * (k + 1) + l];
-        }
-        if (lr) {
-          fi = Ib[12 * (k + 1) + l];
-          if (k + 2 < N) {
-            fz = z[12 * (k + 2) + l];
-            fy = y[12 * (k + 2) + l];
-          }
-        }
+      {
+        const int kn = k + 1 < N ? k + 1 : N - 1, kz = k + 2 < N ? k + 2 : N - 1;
+        adm_pf_load(pf, Rb + ADM_REC * kn, pcode, 0);
+        const int ln = kn < N - 1 ? l17 : l11;
+        fx = x[18 * kn + ln];
+        fq = qs[18 * kn + ln];
+        fi = Ib[12 * kn + l11];
+        fz = z[12 * kz + l11];
+        fy = y[12 * kz + l11];
       }
       if (k < N - 1 && lr) sT1[l] = t1;
       wave_sync();
@@ -522,26 +532,26 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
     // the relaxation of x_{k+1}, and the projection and dual update of block k+1 (block 0 after
     // the sweep).  xt never leaves registers: step k needs only xt_k and xt_{k+1}.  Every global
     // value a lane reads it wrote itself (lane = index within the knot / block).
-    double bw = 0.0, bz = 0.0, by = 0.0, bl = 0.0, bi = 0.0, bx = 0.0, xtp = 0.0;
-    adm_pf_load(pf, Linv + ADM_LP * (N - 1), nullptr, nullptr, l);
-    if (l < 12) bw = wv[18 * (N - 1) + l];
+    double bw, bz = 0.0, by = 0.0, bl = 0.0, bi = 0.0, bx = 0.0, xtp = 0.0;
+    adm_pf_load(pf, Rb + ADM_REC * (N - 1), pcode, 10);
+    bw = wv[18 * (N - 1) + l11];
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
       wave_sync();
-      adm_pf_store(pf, sB, pdst);
+      adm_pf_store(pf, sB, pcode);
       const double we = bw, zr0 = bz, yr0 = by, lr0 = bl, ir0 = bi, xe1 = bx;
-      // step k - 1's loads: its blocks, w_{k-1}, block k's rows, x_k (block 0's rows and x_0 at k = 0)
-      if (k > 0) {
-        adm_pf_load(pf, Linv + ADM_LP * (k - 1), Cb + 216 * (k - 1), Jb + ADM_JC * (k - 1), l);
-        if (lx) bw = wv[18 * (k - 1) + l];
+      // step k - 1's loads: its blocks, w_{k-1}, block k's rows, x_k (block 0's rows and x_0 at
+      // k = 0: there the block loads re-read stage 0, unused)
+      {
+        const int kp = k > 0 ? k - 1 : 0;
+        adm_pf_load(pf, Rb + ADM_REC * kp, pcode, 10);
+        bw = wv[18 * kp + l17];
+        bz = z[12 * k + l11];
+        by = y[12 * k + l11];
+        bl = ls[12 * k + l11];
+        bi = Ib[12 * k + l11];
+        bx = x[18 * k + (k < N - 1 ? l17 : l11)];
       }
-      if (lr) {
-        bz = z[12 * k + l];
-        by = y[12 * k + l];
-        bl = ls[12 * k + l];
-        bi = Ib[12 * k + l];
-      }
-      if (l < nk) bx = x[18 * k + l];
       wave_sync();
       if (l < nk) {
         double r = we;
@@ -597,7 +607,7 @@ __global__ void __launch_bounds__(64) k_admm(AdmmArgs a) {
         rho = rest;
         rv = 1e3 * rho;
         ri = 1.0 / rv;
-        adm_factor(a, N, rho, Pq, Pd, Ib, Jb, Linv, Cb, sS, sJ, sL, sCp, l);
+        adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
       }
     }
   }

@@ -261,12 +261,12 @@ struct Bufs {
 };
 
 // per-problem sizes of the ADMM buffers (doubles), in the order admm_layout lays them out
-constexpr int ADM_NBUF = 19;
+constexpr int ADM_NBUF = 16;
 void admm_sizes(long N, long sz[ADM_NBUF]) {
   const long T = 18 * N - 6, m = 12 * N;
-  const long v[ADM_NBUF] = {T, m, m, T, 1,                                  // x z y q rho (state)
-                            36 * N, T, ADM_JC * (N - 1), m, T, m, T, m, T, m,  // Pq Pd J I qs ls D E Dt Et
-                            ADM_LP * N, 216 * (N - 1), T, T};                  // Linv C w xt
+  const long v[ADM_NBUF] = {T, m, m, T, 1,                        // x z y q rho (state)
+                            36 * N, T, m, T, m, T, m, T, m,         // Pq Pd I qs ls D E Dt Et
+                            ADM_REC * (N + 1), T};                  // stage records, w
   for (int i = 0; i < ADM_NBUF; ++i) sz[i] = v[i];
 }
 // AdmmArgs pointers of problems [b0, ...) in the handle's ADMM allocation (array-of-buffers, each
@@ -282,8 +282,8 @@ AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
   }
   AdmmArgs a{};
   a.sx = p[0]; a.sz = p[1]; a.sy = p[2]; a.sq = p[3]; a.srho = p[4];
-  a.Pq = p[5]; a.Pd = p[6]; a.J = p[7]; a.I = p[8]; a.qs = p[9]; a.ls = p[10]; a.D = p[11]; a.E = p[12];
-  a.Dt = p[13]; a.Et = p[14]; a.Linv = p[15]; a.C = p[16]; a.w = p[17]; a.xt = p[18];
+  a.Pq = p[5]; a.Pd = p[6]; a.I = p[7]; a.qs = p[8]; a.ls = p[9]; a.D = p[10]; a.E = p[11];
+  a.Dt = p[12]; a.Et = p[13]; a.R = p[14]; a.w = p[15];
   a.iters = its + b0 * I7M_MAX_SQP;
   return a;
 }
