@@ -325,8 +325,8 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
            "osqp_iters_per_qp": {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())},
            "qp_iters_mean": float(st["qp_iters"].mean()), "finite": bool(np.isfinite(out).all()),
            "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
-    if "k_admm" in kt:
-        ms, cnt = kt["k_admm"]
+    if "k_admm_iter" in kt:
+        ms, cnt = kt["k_admm_iter"]
         avg_s = ms / max(cnt, 1) / 1e3
         # problems per launch and OSQP iterations per launch (the last step's record)
         ppl = float((it >= 0).sum()) / max(cnt // steps, 1)
@@ -334,8 +334,8 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
         ab = algorithmic_bytes(N)
         achieved = ppl * ab / avg_s / 1e9
         stream_gbs = ipl * admm_bytes_per_iter(N) / avg_s / 1e9
-        res["roofline"] = {"bound": "hbm", "kernel": "k_admm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic("k_admm", B, N),
+        res["roofline"] = {"bound": "hbm", "kernel": "k_admm_iter", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic("k_admm_iter", B, N),
                            "algorithmic_bytes_per_problem": ab, "problems_per_launch": ppl,
                            "avg_launch_us": avg_s * 1e6,
                            "factor_stream": {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,

@@ -76,7 +76,7 @@ extern "C" {
 
 /* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
  * layout, field meaning or enum count changes.  4: I7M_QP_ADMM and i7m_config's admm_* fields
- * (appended), I7M_K_COUNT 9 (I7M_K_ADMM), i7m_admm_reset / i7m_get_admm_stats /
+ * (appended), I7M_K_COUNT 10 (I7M_K_ADMM, I7M_K_ADMM_PREP), i7m_admm_reset / i7m_get_admm_stats /
  * i7m_get_admm_state (0.4 builds).  3: i7m_config's former `pad` is `h2h_chunks` (a
  * nonzero value changes how i7m_solve runs; outside [0, 64] it is refused) and I7M_K_COUNT is 8
  * (I7M_K_LINESEARCH_TAIL added) — size timing arrays from I7M_K_COUNT of this header (0.3 builds).
@@ -290,8 +290,8 @@ int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* en
 
 /* Per-kernel device timing with HIP events on the launch stream. */
 enum { I7M_K_LIN = 0, I7M_K_RICCATI = 1, I7M_K_LINESEARCH = 2, I7M_K_RICCATI_BOX = 3, I7M_K_IPM = 4, I7M_K_IPM_FUSED = 5,
-       I7M_K_SQP_FUSED = 6, I7M_K_LINESEARCH_TAIL = 7 /* second launch of a split line search */, I7M_K_ADMM = 8,
-       I7M_K_COUNT = 9 };
+       I7M_K_SQP_FUSED = 6, I7M_K_LINESEARCH_TAIL = 7 /* second launch of a split line search */, I7M_K_ADMM = 8 /* OSQP iterations */,
+       I7M_K_ADMM_PREP = 9 /* the QP's scaling and factor */, I7M_K_COUNT = 10 };
 int i7m_set_timing(i7m_handle* h, int enable);
 /* Sums (ms) and launch counts per kernel id since the last reset; synchronises. */
 int i7m_get_kernel_times(i7m_handle* h, double* ms_sum, int32_t* counts, int32_t n);

@@ -27,10 +27,10 @@ MAX_N = 64
 LIN_STRIDE, COST_STRIDE = 114, 10
 
 (I7M_K_LIN, I7M_K_RICCATI, I7M_K_LINESEARCH, I7M_K_RICCATI_BOX, I7M_K_IPM, I7M_K_IPM_FUSED, I7M_K_SQP_FUSED,
- I7M_K_LINESEARCH_TAIL, I7M_K_ADMM) = range(9)
-I7M_K_COUNT = 9
+ I7M_K_LINESEARCH_TAIL, I7M_K_ADMM, I7M_K_ADMM_PREP) = range(10)
+I7M_K_COUNT = 10
 KERNEL_NAMES = ("k_linearize", "k_riccati", "k_linesearch", "k_riccati_box", "k_ipm", "k_ipm_fused", "k_sqp_fused",
-                "k_linesearch_tail", "k_admm")
+                "k_linesearch_tail", "k_admm_iter", "k_admm_prep")
 
 
 class I7MError(RuntimeError):

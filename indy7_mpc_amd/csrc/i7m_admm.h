@@ -46,6 +46,7 @@ struct AdmmArgs {
   double *sx, *sz, *sy, *sq, *srho;
   // scratch per problem
   double *Pq, *Pd, *I, *qs, *ls, *D, *E, *Dt, *Et, *R, *w;
+  double* cs;  // (B) OSQP's cost scale c of the current QP (k_admm_prep -> k_admm_iter)
   int* iters;  // (B, I7M_MAX_SQP): OSQP iterations of SQP iteration `sqp_iter`
   int sqp_iter;
   int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
@@ -56,7 +57,10 @@ struct AdmmArgs {
 // (E_i D_i for I, E_i dt D_{6+i} for dt I) and its v rows (6 x 18): 120 of 216.  Staged to LDS
 // unpacked, so the arithmetic is the dense form's (the dropped entries are exact zeros).
 #ifndef I7M_ADMM_WPE
-#define I7M_ADMM_WPE 2  // waves per SIMD k_admm is compiled for (registers: <= 256 / wave at 2)
+#define I7M_ADMM_WPE 2  // waves per SIMD k_admm_prep (and the adaptive-rho iteration kernel) is compiled for
+#endif
+#ifndef I7M_ADMM_ITER_WPE
+#define I7M_ADMM_ITER_WPE 2  // ... and k_admm_iter without adaptive rho (at 3: 78 spilled VGPRs, 30% slower)
 #endif
 constexpr int ADM_LP = 171, ADM_JC = 120;
 // One record per stage, N + 1 per problem: record k = [Linv_k packed (171) | C_{k-1} (216; record
@@ -249,6 +253,166 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
   return true;
 }
 
+// OSQP's scaling of the QP (src/osqp_solver.py:137-143: update(Px), update(Ax) rescale with the
+// previous q; then update(q, l, u)), as oracle/cpp/i7m_cpu.cpp Solver::admm_setup: 10 Ruiz passes
+// on [P A'; A 0] and the cost normalisation, then the scaled P blocks, J_k, the -I entries, q and l
+// into HBM; returns the cost scale c.  D and E live in LDS during the passes; a lane owns columns
+// e = l + 64 t (t < CT) and rows r = l + 64 t (t < 2 CT / 3), whose scale factors and q entries
+// stay in its registers.  Every column's and row's inf-norm reads its entries unconditionally at
+// clamped indices and selects (a P column: 6 entries of the quadratic block or the diagonal; an A
+// column: the -I entry, J's identity / dt entry and 6 linearisation entries; an A row: its -I
+// entry and 18 J entries), so the loads of all of a lane's columns issue together.  The products
+// are the port's (|a_ij| D_j E_i in its order; max is exact), so D, E and c are the one-kernel
+// version's to the bit, the cost sum's wave reduction aside.
+__device__ __forceinline__ double adm_pq(const double* w, int i, int j) { return w[6] * (w[i] * w[j]); }
+template <int CT>
+__device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int T, int m, const double* LIN,
+                                            const double* CO, const double* QD, const double* X, double* qold,
+                                            double* Pq, double* Pd, double* Jb, double* Ib, double* qs, double* ls,
+                                            double* D, double* E, double* sD, double* sE, double* sDt, int l) {
+  constexpr int RT = 2 * CT / 3;
+  const double dt = a.P.dt;
+  double qv[CT], etv[RT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int e = l + 64 * t;
+    qv[t] = 0.0;
+    if (e < T) {
+      sD[e] = 1.0;
+      qv[t] = qold[e];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+    if (l + 64 * t < m) sE[l + 64 * t] = 1.0;
+  wave_sync();
+  double c = 1.0;
+  // the P part of column e's inf-norm (knot k, index j in the knot): max_i |P_ij| D_i D_j c
+  auto pcol = [&](const double* Cp, int k, int j, double dj) {
+    const double* w = Cp + COST_STRIDE * k;
+    const int jq = j < 6 ? j : 0;
+    double mq = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) mq = fmax(mq, fabs(adm_pq(w, i, jq)) * (sD[18 * k + i] * dj) * c);
+    const double pd = j < 12 ? w[7] : w[8];
+    return j < 6 ? mq : fabs(pd) * (dj * dj) * c;
+  };
+  for (int pass = 0; pass < a.A.scaling; ++pass) {
+    // every pass recomputes its indices (hoisted out of the pass loop they would take ~300 VGPRs)
+    const double* Lp = LIN;
+    const double* Cp = CO;
+    int lp = l;
+    asm volatile("" : "+v"(lp));
+#pragma unroll 3
+    for (int t = 0; t < CT; ++t) {
+      const int e = min(lp + 64 * t, T - 1), k = e / 18, j = e - 18 * k;
+      const double dj = sD[e];
+      double mx = pcol(Cp, k, j, dj);
+      const double ei = sE[12 * k + (j < 12 ? j : 0)] * dj;
+      if (j < 12) mx = fmax(mx, ei);
+      // J_k's column j (rows of block k + 1; the last knot has none): the identity / dt entry, 6
+      // linearisation entries
+      const int kk = k < N - 1 ? k : N - 2;
+      const double* L = Lp + LIN_STRIDE * kk;
+      const double* Eb = sE + 12 * (kk + 1);
+      const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
+      const double eid = Eb[j < 6 ? j : (j < 12 ? j - 6 : 0)] * (j < 6 ? 1.0 : dt) * dj;
+      double mj = j < 12 ? eid : 0.0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) mj = fmax(mj, Eb[6 + r] * fabs(L[jb + 6 * r]) * dj);
+      if (k < N - 1) mx = fmax(mx, mj);
+      sDt[lp + 64 * t] = 1.0 / sqrt(adm_limit(mx));
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const int r = min(lp + 64 * t, m - 1), blk = r / 12, i = r - 12 * blk;
+      const double er = sE[r];
+      double mx = er * sD[18 * blk + i];
+      // row i of J_{blk-1} (block 0's rows are -I on x_0 alone)
+      const int kk = blk > 0 ? blk - 1 : 0;
+      const double* L = Lp + LIN_STRIDE * kk;
+      const double* Db = sD + 18 * kk;
+      // rows 0-5: the identity and dt entries; rows 6-11: 18 linearisation entries
+      const int i6 = i < 6 ? i : i - 6;
+      const double mi = fmax(er * 1.0 * Db[i6], er * dt * Db[6 + i6]);
+      double ml = 0.0;
+#pragma unroll
+      for (int j = 0; j < 18; ++j) {
+        const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
+        ml = fmax(ml, er * fabs(L[jb + 6 * i6]) * Db[j]);
+      }
+      const double mj = i < 6 ? mi : ml;
+      if (blk > 0) mx = fmax(mx, mj);
+      etv[t] = 1.0 / sqrt(adm_limit(mx));
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int e = lp + 64 * t;
+      const double dtt = sDt[e];
+      if (e < T) sD[e] = sD[e] * dtt;
+      qv[t] = dtt * qv[t];
+    }
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+      if (lp + 64 * t < m) sE[lp + 64 * t] = sE[lp + 64 * t] * etv[t];
+    wave_sync();
+    // cost normalisation: mean column norm of the scaled P, |q|
+    double sm = 0.0, qm = 0.0;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int e = lp + 64 * t, ec = min(e, T - 1), k = ec / 18, j = ec - 18 * k;
+      const double mx = pcol(Cp, k, j, sD[ec]);
+      if (e < T) {
+        sm += mx;
+        qm = fmax(qm, fabs(qv[t]));
+      }
+    }
+    sm = adm_wave_sum(sm);
+    qm = adm_limit(adm_wave_max(qm));
+    const double ct = 1.0 / adm_limit(fmax(sm / T, qm));
+#pragma unroll
+    for (int t = 0; t < CT; ++t) qv[t] = qv[t] * ct;
+    c = c * ct;
+  }
+  // scaled data: P <- c D P D, J <- E J D, I <- -E D, q <- c D g (update(q)), l <- E l
+  for (int e = l; e < T; e += 64) D[e] = sD[e];
+  for (int r = l; r < m; r += 64) E[r] = sE[r];
+#pragma unroll 4
+  for (int x = l; x < 36 * N; x += 64) {
+    const int k = x / 36, q = x - 36 * k, i = q / 6, j = q - 6 * i;
+    Pq[x] = adm_pq(CO + COST_STRIDE * k, i, j) * (sD[18 * k + i] * sD[18 * k + j]) * c;
+  }
+#pragma unroll 4
+  for (int x = l; x < 120 * (N - 1); x += 64) {
+    const int k = x / 120, e = x - 120 * k;
+    int i, j;
+    if (e < 6) { i = e; j = e; }
+    else if (e < 12) { i = e - 6; j = e; }
+    else { i = 6 + (e - 12) / 18; j = (e - 12) % 18; }
+    Jb[ADM_REC * k + e] = sE[12 * (k + 1) + i] * adm_jk(LIN + LIN_STRIDE * k, dt, i, j) * sD[18 * k + j];
+  }
+  for (int r = l; r < m; r += 64) {
+    const int k = r / 12, i = r - 12 * k;
+    Ib[r] = -sE[r] * sD[18 * k + i];
+    double lv;
+    if (k == 0) lv = -a.xs[12 * (long)b + i];
+    else lv = i < 6 ? 0.0 : -QD[QPD_STRIDE * (k - 1) + QPD_CV + i - 6];
+    ls[r] = sE[r] * lv;
+  }
+  for (int e = l; e < T; e += 64) {
+    const int k = e / 18, j = e - 18 * k;
+    const double* w = CO + COST_STRIDE * k;
+    const double dd = sD[e];
+    Pd[e] = j < 6 ? 0.0 : (j < 12 ? w[7] : w[8]) * (dd * dd) * c;
+    const double g = j < 6 ? w[6] * w[j] : (j < 12 ? w[7] * X[e] : w[8] * X[e]);
+    qold[e] = g;
+    qs[e] = c * (dd * g);
+  }
+  wave_sync_all();
+  return c;
+}
+
 // M = P + sigma I + A' rho A, block Cholesky with inverted diagonal factors (as Solver::
 // admm_factor of the port): Linv_k (packed) into record k, C_k into record k+1
 __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
@@ -326,12 +490,19 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
   }
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_WPE, I7M_ADMM_WPE))) k_admm(AdmmArgs a) {
+// The QP in two launches: k_admm_prep (PH 1: scaling, the new q and l, the factor; c to a.cs) and
+// k_admm_iter (PH 2: OSQP's iterations and the output; PH 4: with adaptive rho, whose re-factor
+// needs the factor's registers and LDS — without it the iteration kernel is compiled lean).
+template <int PH, int CT>
+__device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   const int b = a.b0 + blockIdx.x;
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
-  __shared__ double sB[324 + 216 + 216], sS[324], sCp[216], sR[32], sW[32], sT0[16], sT1[16];
+  constexpr bool FAC = (PH & 1) || (PH & 4);
+  // (k_admm_prep: sB holds the column scale factors of a Ruiz pass before the factor needs it)
+  __shared__ double sB[(PH & 1) && 64 * CT > 756 ? 64 * CT : 756], sS[FAC ? 324 : 1], sCp[FAC ? 216 : 1], sR[32], sW[32], sT0[16], sT1[16];
+  __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1];
   double* sL = sB;
   double* sC = sB + 324;
   double* sJ = sB + 540;
@@ -352,118 +523,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
   double* ls = a.ls + (long)b * m;
   double* D = a.D + (long)b * T;
   double* E = a.E + (long)b * m;
-  double* Dt = a.Dt + (long)b * T;
-  double* Et = a.Et + (long)b * m;
 
   double* wv = a.w + (long)b * T;
   const double dt = P.dt;
 
-  // ---- 1. unscaled P blocks (src/osqp_solver.py:103-135), the previous q, D = E = 1
-  for (int k = 0; k < N; ++k) {
-    const double* w = CO + COST_STRIDE * k;
-    if (l < 36) Pq[36 * k + l] = w[6] * (w[l / 6] * w[l % 6]);
-    if (l < 18 && 18 * k + l < T) Pd[18 * k + l] = l < 6 ? 0.0 : (l < 12 ? w[7] : w[8]);
-  }
-  for (int e = l; e < T; e += 64) { qs[e] = qold[e]; D[e] = 1.0; }
-  for (int r = l; r < m; r += 64) E[r] = 1.0;
-  wave_sync_all();
   double c = 1.0;
-  for (int pass = 0; pass < a.A.scaling; ++pass) {
-    // column inf-norms of the scaled [P; A] and row inf-norms of the scaled A
-    for (int k = 0; k < N; ++k) {
-      const int nk = k < N - 1 ? 18 : 12;
-      const double* L = LIN + LIN_STRIDE * k;
-      if (l < nk) {
-        const int j = l, e = 18 * k + j;
-        const double dj = D[e];
-        double mx = 0.0;
-        if (j < 6) {
-          for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(Pq[36 * k + 6 * i + j]) * (D[18 * k + i] * dj) * c);
-        } else {
-          mx = fabs(Pd[e]) * (dj * dj) * c;
-        }
-        if (j < 12) mx = fmax(mx, E[12 * k + j] * dj);
-        if (k < N - 1)
-          for (int i = 0; i < 12; ++i) mx = fmax(mx, E[12 * (k + 1) + i] * fabs(adm_jk(L, dt, i, j)) * dj);
-        Dt[e] = 1.0 / sqrt(adm_limit(mx));
-      } else if (l >= 32 && l < 44 && k < N - 1) {
-        const int i = l - 32, r = 12 * (k + 1) + i;
-        const double er = E[r];
-        double mx = er * D[18 * (k + 1) + i];
-        for (int j = 0; j < 18; ++j) mx = fmax(mx, er * fabs(adm_jk(L, dt, i, j)) * D[18 * k + j]);
-        Et[r] = 1.0 / sqrt(adm_limit(mx));
-      } else if (l >= 48 && l < 60 && k == 0) {
-        const int i = l - 48;
-        Et[i] = 1.0 / sqrt(adm_limit(E[i] * D[i]));
-      }
-    }
-    wave_sync_all();
-    for (int e = l; e < T; e += 64) { D[e] = D[e] * Dt[e]; qs[e] = Dt[e] * qs[e]; }
-    for (int r = l; r < m; r += 64) E[r] = E[r] * Et[r];
-    wave_sync_all();
-    // cost normalisation: mean column norm of the scaled P, |q|
-    double s = 0.0, qm = 0.0;
-    for (int e = l; e < T; e += 64) {
-      const int k = e / 18, j = e - 18 * k;
-      double mx;
-      if (j < 6) {
-        mx = 0.0;
-        for (int i = 0; i < 6; ++i) mx = fmax(mx, fabs(Pq[36 * k + 6 * i + j]) * (D[18 * k + i] * D[e]) * c);
-      } else {
-        mx = fabs(Pd[e]) * (D[e] * D[e]) * c;
-      }
-      s += mx;
-      qm = fmax(qm, fabs(qs[e]));
-    }
-    s = adm_wave_sum(s);
-    qm = adm_limit(adm_wave_max(qm));
-    const double ct = 1.0 / adm_limit(fmax(s / T, qm));
-    for (int e = l; e < T; e += 64) qs[e] = qs[e] * ct;
-    c = c * ct;
-    wave_sync_all();
-  }
-  // scaled data: P <- c D P D, J <- E J D, I <- -E D, q <- c D g (update(q)), l <- E l
-  for (int k = 0; k < N; ++k) {
-    if (l < 36) {
-      const int i = l / 6, j = l % 6;
-      Pq[36 * k + l] = Pq[36 * k + l] * (D[18 * k + i] * D[18 * k + j]) * c;
-    }
-    if (l >= 6 && l < 18 && 18 * k + l < T) {
-      const int e = 18 * k + l;
-      Pd[e] = Pd[e] * (D[e] * D[e]) * c;
-    }
-    if (k < N - 1) {
-      const double* L = LIN + LIN_STRIDE * k;
-      double* Jc = Jb + ADM_REC * k;
-      for (int e = l; e < ADM_JC; e += 64) {
-        int i, j;
-        if (e < 6) { i = e; j = e; }
-        else if (e < 12) { i = e - 6; j = e; }
-        else { i = 6 + (e - 12) / 18; j = (e - 12) % 18; }
-        Jc[e] = E[12 * (k + 1) + i] * adm_jk(L, dt, i, j) * D[18 * k + j];
-      }
-    }
-  }
-  for (int r = l; r < m; r += 64) {
-    const int k = r / 12, i = r - 12 * k;
-    Ib[r] = -E[r] * D[18 * k + i];
-    double lv;
-    if (k == 0) lv = -a.xs[12 * (long)b + i];
-    else lv = i < 6 ? 0.0 : -QD[QPD_STRIDE * (k - 1) + QPD_CV + i - 6];
-    ls[r] = E[r] * lv;
-  }
-  for (int e = l; e < T; e += 64) {
-    const int k = e / 18, j = e - 18 * k;
-    const double* w = CO + COST_STRIDE * k;
-    const double g = j < 6 ? w[6] * w[j] : (j < 12 ? w[7] * X[e] : w[8] * X[e]);
-    qold[e] = g;
-    qs[e] = c * (D[e] * g);
-  }
-  wave_sync_all();
+  if constexpr (PH & 1) {
+  c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
 
   // ---- 2. factor
+#ifndef I7M_DIAG_ADMM_NOFACTOR  // (timing builds only: the prep kernel without its factor)
+  adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+#endif
+  if (l == 0) a.cs[b] = c;
+  }
+  if constexpr (PH & 2) {
+  if constexpr (!(PH & 1)) {
+    // the LDS slots no sweep step writes (Linv's upper triangle, J's q-row zeros) are zeros
+    for (int e = l; e < 324 + 216 + 216; e += 64) sB[e] = 0.0;
+  }
+  c = a.cs[b];
   double rho = a.srho[b];
-  adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
   double rv = 1e3 * rho, ri = 1.0 / rv;
   const double al = a.A.alpha, sg = a.A.sigma;
 
@@ -473,7 +553,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
   // its vector entries (x, q, the -I entries, z, y, l of the rows it finishes) — is loaded into
   // registers at the start of this step, before this step's stores, so the loads' latency hides
   // behind the step and waiting for them never waits for a store (vmcnt is in order).  The LDS
-  // slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set by the factor.
+  // slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set above.
   int pcode[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) pcode[t] = adm_pf_code(l + 64 * t);
@@ -603,11 +683,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
         solved = true;
         break;
       }
-      if (adapt && (rest > rho * a.A.adapt_tol || rest < rho / a.A.adapt_tol)) {
-        rho = rest;
-        rv = 1e3 * rho;
-        ri = 1.0 / rv;
-        adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+      if constexpr (PH & 4) {
+        if (adapt && (rest > rho * a.A.adapt_tol || rest < rho / a.A.adapt_tol)) {
+          rho = rest;
+          rv = 1e3 * rho;
+          ri = 1.0 / rv;
+          adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+        }
       }
     }
   }
@@ -618,6 +700,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
   }
   double* so = a.sol + (long)b * T;
   for (int e = l; e < T; e += 64) so[e] = D[e] * x[e];
+  }
+}
+
+template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_WPE, I7M_ADMM_WPE))) k_admm_prep(AdmmArgs a) {
+  admm_body<1, CT>(a);
+}
+template <bool ADAPT>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ADAPT ? I7M_ADMM_WPE : I7M_ADMM_ITER_WPE,
+                                                                       ADAPT ? I7M_ADMM_WPE : I7M_ADMM_ITER_WPE)))
+k_admm_iter(AdmmArgs a) {
+  admm_body<ADAPT ? 6 : 2, 1>(a);
 }
 
 }  // namespace i7m

@@ -261,12 +261,12 @@ struct Bufs {
 };
 
 // per-problem sizes of the ADMM buffers (doubles), in the order admm_layout lays them out
-constexpr int ADM_NBUF = 16;
+constexpr int ADM_NBUF = 15;
 void admm_sizes(long N, long sz[ADM_NBUF]) {
   const long T = 18 * N - 6, m = 12 * N;
   const long v[ADM_NBUF] = {T, m, m, T, 1,                        // x z y q rho (state)
-                            36 * N, T, m, T, m, T, m, T, m,         // Pq Pd I qs ls D E Dt Et
-                            ADM_REC * (N + 1), T};                  // stage records, w
+                            36 * N, T, m, T, m, T, m,               // Pq Pd I qs ls D E
+                            ADM_REC * (N + 1), T, 1};               // stage records, w, c
   for (int i = 0; i < ADM_NBUF; ++i) sz[i] = v[i];
 }
 // AdmmArgs pointers of problems [b0, ...) in the handle's ADMM allocation (array-of-buffers, each
@@ -283,7 +283,7 @@ AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
   AdmmArgs a{};
   a.sx = p[0]; a.sz = p[1]; a.sy = p[2]; a.sq = p[3]; a.srho = p[4];
   a.Pq = p[5]; a.Pd = p[6]; a.I = p[7]; a.qs = p[8]; a.ls = p[9]; a.D = p[10]; a.E = p[11];
-  a.Dt = p[12]; a.Et = p[13]; a.R = p[14]; a.w = p[15];
+  a.R = p[12]; a.w = p[13]; a.cs = p[14];
   a.iters = its + b0 * I7M_MAX_SQP;
   return a;
 }
@@ -524,8 +524,18 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
     for (int lo = 0; lo < P.B; lo += chunk) {
       a.b0 = lo;
       const int n = std::min(chunk, P.B - lo);
-      const int rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
-        hipExtLaunchKernelGGL(k_admm, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+      int rc2 = timed(h, s, I7M_K_ADMM_PREP, [&](hipEvent_t ea, hipEvent_t eb) {
+        if (P.N <= 32)
+          hipExtLaunchKernelGGL(k_admm_prep<9>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+        else
+          hipExtLaunchKernelGGL(k_admm_prep<18>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+      });
+      if (rc2) return rc2;
+      rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
+        if (a.A.adapt_interval)
+          hipExtLaunchKernelGGL(k_admm_iter<true>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+        else
+          hipExtLaunchKernelGGL(k_admm_iter<false>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
       });
       if (rc2) return rc2;
     }

@@ -123,3 +123,21 @@ def test_admm_drop_in_surfaces(lib, model):
     b.resetLambda()
     b.resetRho()
     b.reset()
+
+
+def test_admm_chunked_host_to_host_equals_one_piece(lib, model):
+    """i7m_solve's chunked host-to-host pipeline (h2h_chunks = 3) hands each chunk its own rows of
+    the OSQP state: two consecutive solves equal a one-piece handle's bit for bit, state included."""
+    N, B = 16, 600
+    xcur, goals, XU = synthetic_batch(B, N, 47)
+    h1 = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, h2h_chunks=1)
+    h3 = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, h2h_chunks=3)
+    a1, _ = h1.solve(xcur, goals, XU)
+    a3, _ = h3.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(a1, a3)
+    b1, _ = h1.solve(xcur, goals, a1)
+    b3, _ = h3.solve(xcur, goals, a3)
+    np.testing.assert_array_equal(b1, b3)
+    for u, v in zip(h1.admm_state(B), h3.admm_state(B)):
+        np.testing.assert_array_equal(u, v)
+    np.testing.assert_array_equal(h1.admm_stats(B)[0], h3.admm_stats(B)[0])

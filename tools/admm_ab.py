@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--chunks", default="0,2048,1024")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--scaling", type=int, default=None, help="OSQP's Ruiz passes (default: the reference's 10)")
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -32,7 +33,8 @@ def main():
     for rep in range(2):
         for c in [int(x) for x in a.chunks.split(",")]:
             os.environ["I7M_ADMM_CHUNK"] = str(c)
-            h = _lib.Handle(model, N=a.N, max_batch=a.B, qp_mode=_lib.QP_ADMM)
+            kw = {} if a.scaling is None else {"admm": {"scaling": a.scaling}}
+            h = _lib.Handle(model, N=a.N, max_batch=a.B, qp_mode=_lib.QP_ADMM, **kw)
             xcur, goals, XU = make_batch(h, model, a.B, a.N, seed=45)
             t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
             t_out = torch.empty_like(t_xu)
