@@ -59,6 +59,15 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_WPE
 #define I7M_ADMM_WPE 2  // waves per SIMD k_admm_prep (and the adaptive-rho iteration kernel) is compiled for
 #endif
+#ifndef I7M_ADMM_FACTOR
+#define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
+#endif
+#ifndef I7M_ADMM_SCALE_WPE
+#define I7M_ADMM_SCALE_WPE 2
+#endif
+#ifndef I7M_ADMM_FACTOR_WPE
+#define I7M_ADMM_FACTOR_WPE 2
+#endif
 #ifndef I7M_ADMM_ITER_WPE
 #define I7M_ADMM_ITER_WPE 2  // ... and k_admm_iter without adaptive rho (at 3: 78 spilled VGPRs, 30% slower)
 #endif
@@ -139,6 +148,21 @@ __device__ __forceinline__ double adm_dot(double init, const double* a, int sa, 
   for (int i = 0; i < n; ++i) {
     av[i] = a[sa * i];
     bv[i] = b[i];
+  }
+  double acc = init;
+#pragma unroll
+  for (int i = 0; i < n; ++i) acc += av[i] * bv[i];
+  return acc;
+}
+
+// ... with both operands strided
+template <int n>
+__device__ __forceinline__ double adm_dot2(double init, const double* a, int sa, const double* b, int sb) {
+  double av[n], bv[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    av[i] = a[sa * i];
+    bv[i] = b[sb * i];
   }
   double acc = init;
 #pragma unroll
@@ -414,8 +438,115 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 }
 
 // M = P + sigma I + A' rho A, block Cholesky with inverted diagonal factors (as Solver::
-// admm_factor of the port): Linv_k (packed) into record k, C_k into record k+1
+// admm_factor of the port): Linv_k (packed) into record k, C_k into record k+1.  Per stage: the
+// block S_k in LDS (all lanes, every dot product's operands loaded before its fma chain), its
+// right-looking Cholesky with row i in lane i's registers (the pivot by readlane, the column
+// through LDS: one round trip per pivot), Linv_k by forward substitution with column j in lane j's
+// registers, then C_k.  The last knot's 12 x 12 block is factored padded with an identity, whose
+// entries are stored as the zeros the port has there.  Same operations in the port's order (the
+// zeros the padding and the triangles add are exact).
+__device__ __forceinline__ double adm_readlane(double v, int lane) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)u, lane), hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
+                           double* Rb, double* sS, double* sJ, double* sL, double* sCp, int l0) {
+  const double re = 1e3 * rho, sigma = a.A.sigma;
+  const int T = 18 * N - 6;
+  double* sCol = sL + 324;  // (the sweeps' C slot, free while factoring)
+  for (int k = 0; k < N; ++k) {
+    const int nk = k < N - 1 ? 18 : 12;
+    // every stage recomputes the lane's indices (hoisted out of the stage loop they would take
+    // more registers than the kernel has)
+    int l = l0;
+    asm volatile("" : "+v"(l));
+    const int lr = l < 18 ? l : 17;  // lanes 18-63 shadow lane 17 (never read back)
+    if (k < N - 1) adm_stage_J(sJ, Rb + ADM_REC * k + REC_J, l);
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int e = l + 64 * t;
+      if (e < 324) {
+        const int i = e / 18, j = e - 18 * i, ic = i < 12 ? i : 11, jc = j < 12 ? j : 11;
+        const double pq = Pq[36 * k + 6 * (i < 6 ? i : 0) + (j < 6 ? j : 0)];
+        const double pd = Pd[min(18 * k + i, T - 1)];
+        const double ib = Ib[12 * k + ic];
+        const double dj = adm_dot2<12>(0.0, sJ + i, 18, sJ + j, 18);
+        const double dc = adm_dot2<18>(0.0, sCp + 18 * ic, 1, sCp + 18 * jc, 1);
+        double v = i < 6 && j < 6 ? pq : (i == j && i >= 6 ? pd : 0.0);
+        if (i == j) v += sigma;
+        if (i == j && i < 12) v += re * (ib * ib);
+        if (k < N - 1) v += re * dj;
+        if (k > 0 && i < 12 && j < 12) v -= dc;
+        if (i >= nk || j >= nk) v = i == j ? 1.0 : 0.0;
+        sS[e] = v;
+      }
+    }
+    wave_sync();
+    double r[18];
+#pragma unroll
+    for (int j = 0; j < 18; ++j) r[j] = sS[18 * lr + j];
+#pragma unroll
+    for (int p = 0; p < 18; ++p) {
+      const double d = sqrt(adm_readlane(r[p], p));
+      const double id = 1.0 / d;
+      r[p] = l == p ? d : (l > p ? r[p] * id : r[p]);
+      if (p < 17) {
+        // column p of L to the wave through LDS (double-buffered: no wait for the last reads)
+        double* col = sCol + 32 * (p & 1);
+        if (l < 18) col[l] = r[p];
+        wave_sync();
+#pragma unroll
+        for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
+      }
+    }
+    wave_sync();  // every lane has read S before L overwrites it
+    if (l < 18) {
+#pragma unroll
+      for (int j = 0; j < 18; ++j) sS[18 * l + j] = r[j];
+    }
+    wave_sync();
+    double x[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+      // row i of L is read once x_{i-2} exists (two rows of loads in flight, not all 171)
+      int o = 18 * i;
+      if (i >= 2) asm volatile("" : "+v"(o) : "v"(x[i - 2]));
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < i; ++q) acc += sS[o + q] * x[q];
+      x[i] = ((i == lr ? 1.0 : 0.0) - acc) / sS[o + i];
+    }
+    if (l < 18) {
+#pragma unroll
+      for (int i = 0; i < 18; ++i) {
+        const double v = i < nk && l < nk ? x[i] : 0.0;
+        sL[18 * i + l] = v;
+        if (i >= l) Rb[ADM_REC * k + adm_tri(i, l)] = v;
+      }
+    }
+    wave_sync();
+    if (k < N - 1) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int e = l + 64 * t;
+        if (e < 216) {
+          const int i = e / 18, j = e - 18 * i;
+          const double acc = adm_dot2<18>(0.0, sJ + 18 * i, 1, sL + 18 * j, 1);
+          const double cv = re * Ib[12 * (k + 1) + i] * acc;
+          sCp[e] = cv;
+          Rb[ADM_REC * (k + 1) + REC_C + e] = cv;
+        }
+      }
+    }
+    wave_sync_all();
+  }
+}
+
+// The factor with every step's operands through LDS (the kernel before the register Cholesky;
+// I7M_ADMM_FACTOR 1, A/B builds)
+__device__ void adm_factor_lds(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
                            double* Rb, double* sS, double* sJ, double* sL, double* sCp,
                            int l) {
   const double re = 1e3 * rho, sigma = a.A.sigma;
@@ -490,18 +621,19 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
   }
 }
 
-// The QP in two launches: k_admm_prep (PH 1: scaling, the new q and l, the factor; c to a.cs) and
-// k_admm_iter (PH 2: OSQP's iterations and the output; PH 4: with adaptive rho, whose re-factor
-// needs the factor's registers and LDS — without it the iteration kernel is compiled lean).
+// The QP in three launches: k_admm_scale (PH 1: scaling, the new q and l; c to a.cs), k_admm_factor
+// (PH 8: the block Cholesky) and k_admm_iter (PH 2: OSQP's iterations and the output; PH 4: with
+// adaptive rho, whose re-factor needs the factor's registers and LDS — without it the iteration
+// kernel is compiled lean).  Each is compiled for its own registers and LDS.
 template <int PH, int CT>
 __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   const int b = a.b0 + blockIdx.x;
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
-  constexpr bool FAC = (PH & 1) || (PH & 4);
+  constexpr bool FAC = (PH & 8) || (PH & 4);
   // (k_admm_prep: sB holds the column scale factors of a Ruiz pass before the factor needs it)
-  __shared__ double sB[(PH & 1) && 64 * CT > 756 ? 64 * CT : 756], sS[FAC ? 324 : 1], sCp[FAC ? 216 : 1], sR[32], sW[32], sT0[16], sT1[16];
+  __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 324 : 1], sCp[FAC ? 216 : 1], sR[32], sW[32], sT0[16], sT1[16];
   __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1];
   double* sL = sB;
   double* sC = sB + 324;
@@ -529,13 +661,15 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
 
   double c = 1.0;
   if constexpr (PH & 1) {
-  c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
-
-  // ---- 2. factor
-#ifndef I7M_DIAG_ADMM_NOFACTOR  // (timing builds only: the prep kernel without its factor)
-  adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+    c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
+    if (l == 0) a.cs[b] = c;
+  }
+  if constexpr (PH & 8) {
+#if I7M_ADMM_FACTOR == 1
+    adm_factor_lds(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+#else
+    adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
 #endif
-  if (l == 0) a.cs[b] = c;
   }
   if constexpr (PH & 2) {
   if constexpr (!(PH & 1)) {
@@ -704,8 +838,13 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
 }
 
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_WPE, I7M_ADMM_WPE))) k_admm_prep(AdmmArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_SCALE_WPE, I7M_ADMM_SCALE_WPE)))
+k_admm_scale(AdmmArgs a) {
   admm_body<1, CT>(a);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_FACTOR_WPE, I7M_ADMM_FACTOR_WPE)))
+k_admm_factor(AdmmArgs a) {
+  admm_body<8, 1>(a);
 }
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ADAPT ? I7M_ADMM_WPE : I7M_ADMM_ITER_WPE,

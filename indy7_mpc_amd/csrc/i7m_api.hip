@@ -525,10 +525,12 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
       a.b0 = lo;
       const int n = std::min(chunk, P.B - lo);
       int rc2 = timed(h, s, I7M_K_ADMM_PREP, [&](hipEvent_t ea, hipEvent_t eb) {
+        // scaling, then the factor (one event pair around both)
         if (P.N <= 32)
-          hipExtLaunchKernelGGL(k_admm_prep<9>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+          hipExtLaunchKernelGGL(k_admm_scale<9>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
         else
-          hipExtLaunchKernelGGL(k_admm_prep<18>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+          hipExtLaunchKernelGGL(k_admm_scale<18>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
+        hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
       });
       if (rc2) return rc2;
       rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
