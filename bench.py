@@ -266,7 +266,7 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
 
 
 def admm_bytes_per_iter(N: int):
-    """HBM bytes one OSQP iteration of k_admm streams per problem (i7m_admm.h): the forward and the
+    """HBM bytes one OSQP iteration of k_admm_iter streams per problem (i7m_admm.h): the forward and the
     backward sweep each read every stage's packed Linv (171), coupling C (216) and compact scaled J
     (120) doubles, plus the per-knot vectors (x, q, z, y, w, xt and the scaling rows: ~120 doubles
     per knot)."""
@@ -276,7 +276,7 @@ def admm_bytes_per_iter(N: int):
 def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 32, native=None,
                  cpu_budget: float = 10.0, cpu_threads: int = 1):
     """Config 3's problems (B = 4096, N = 32) with the QP solved by OSQP's own algorithm on the
-    device (I7M_QP_ADMM, k_admm) — the reference's solver (src/osqp_solver.py:38-40, 137-143).
+    device (I7M_QP_ADMM, k_admm_scale / _factor / _iter) — the reference's solver (src/osqp_solver.py:38-40, 137-143).
     Reported beside the headline (which solves each QP exactly).  Every timed step starts from a
     fresh OSQP state (i7m_admm_reset outside the timed region, the step itself timed by HIP events
     on the solve stream): the reference's first solve, its hardest.  With `native` (rank 0, N = 1)

@@ -6,7 +6,7 @@
 // first 12 goal distances of notebooks/pin_mpc_indy7.ipynb cell 2 to 1e-9); the C++ port
 // (oracle/cpp/i7m_cpu.cpp, Solver::admm) runs it in the block form this kernel runs.
 //
-// k_admm: one wavefront per problem, the whole QP in one launch:
+// One wavefront per problem, the QP in three launches (k_admm_scale, k_admm_factor, k_admm_iter):
 //   1. OSQP's Ruiz equilibration (10 passes) of [P A'; A 0] with the previous QP's q (the
 //      reference re-scales inside update(Ax), before update(q)), then the new q = c D g and
 //      l = u = E l;
@@ -57,13 +57,13 @@ struct AdmmArgs {
 // (E_i D_i for I, E_i dt D_{6+i} for dt I) and its v rows (6 x 18): 120 of 216.  Staged to LDS
 // unpacked, so the arithmetic is the dense form's (the dropped entries are exact zeros).
 #ifndef I7M_ADMM_WPE
-#define I7M_ADMM_WPE 2  // waves per SIMD k_admm_prep (and the adaptive-rho iteration kernel) is compiled for
+#define I7M_ADMM_WPE 2  // waves per SIMD the adaptive-rho iteration kernel is compiled for
 #endif
 #ifndef I7M_ADMM_FACTOR
 #define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
 #ifndef I7M_ADMM_SCALE_WPE
-#define I7M_ADMM_SCALE_WPE 2
+#define I7M_ADMM_SCALE_WPE 3  // (127 VGPRs, 12 KB LDS: 3 waves per SIMD; 2.11 -> 2.08 ms prep)
 #endif
 #ifndef I7M_ADMM_FACTOR_WPE
 #define I7M_ADMM_FACTOR_WPE 2

@@ -4,7 +4,7 @@ Same constructor, attributes and methods.  The numbers come from the GPU:
   * ``setup_and_solve_qp`` linearises on the device (k_linearize) and solves the QP EXACTLY
     with the block-tridiagonal Riccati kernel (k_riccati).  The reference hands the same
     P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.  With
-    ``qp_mode="admm"`` it runs OSQP's algorithm itself (k_admm, i7m_admm.h) from a warm-started
+    ``qp_mode="admm"`` it runs OSQP's algorithm itself (k_admm_scale, k_admm_factor, k_admm_iter; i7m_admm.h) from a warm-started
     per-problem OSQP state, as the reference's ``self.osqp`` object does (:38-40, 140-143): the
     trajectories are then the reference's own (oracle/osqp_admm.py pins them against the
     notebook's printed closed loop).

@@ -4,7 +4,7 @@ oracle/osqp_admm.py restates OSQP (scaling, warm start, termination with the dua
 and is pinned by the reference's own output: the closed loop the notebook prints
 (notebooks/pin_mpc_indy7.ipynb cell 2, tests/golden/notebook_kats.json "mpc_trace").  The C++
 port (oracle/cpp/i7m_cpu.cpp ``admm``) runs the same algorithm in the block form the GPU's
-k_admm uses, and is checked against the numpy restatement here.
+the device kernels use, and is checked against the numpy restatement here.
 """
 import json
 import os

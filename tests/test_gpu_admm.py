@@ -1,4 +1,4 @@
-"""ADMM mode on the GPU (I7M_QP_ADMM, k_admm): OSQP's algorithm — the reference's QP solver,
+"""ADMM mode on the GPU (I7M_QP_ADMM, k_admm_scale / k_admm_factor / k_admm_iter): OSQP's algorithm — the reference's QP solver,
 src/osqp_solver.py:38-40, 137-143 — with its warm-started per-problem state, through the C-ABI.
 
 Checked against the C++ port's ADMM mode (oracle/cpp/i7m_cpu.cpp, the same block form; itself

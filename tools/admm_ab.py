@@ -1,5 +1,5 @@
 """A/B of the ADMM mode's launch shape (I7M_ADMM_CHUNK, read at handle creation): cold OSQP
-state every step, B problems at horizon N, k_admm time per launch and solves/s, one JSON line
+state every step, B problems at horizon N, ADMM kernels' time per launch and solves/s, one JSON line
 per setting.
 
     python tools/admm_ab.py [--B 4096] [--N 32] [--chunks 0,2048,1024] [--steps 3]
