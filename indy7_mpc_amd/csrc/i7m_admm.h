@@ -59,6 +59,9 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_WPE
 #define I7M_ADMM_WPE 2  // waves per SIMD the adaptive-rho iteration kernel is compiled for
 #endif
+#ifndef I7M_ADMM_DOT_CHAINS
+#define I7M_ADMM_DOT_CHAINS 2  // fma chains per sweep dot product (adm_dot)
+#endif
 #ifndef I7M_ADMM_FACTOR
 #define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
@@ -137,8 +140,9 @@ __device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, con
   }
 }
 
-// init + sum_i a[sa i] b[i] over n LDS operands, summed in i order: every operand read is issued
-// before the fma chain, so the chain pays one LDS latency instead of one per term (the dot
+// init + sum_i a[sa i] b[i] over n LDS operands (the sweeps' dot products): every operand read is
+// issued before the fma chains, so they pay one LDS latency instead of one per term; the terms are
+// summed in i order (I7M_ADMM_DOT_CHAINS 1) or as two interleaved chains (2) (the dot
 // products of the sweeps run over fixed lengths; Linv's upper triangle and the padding of the
 // last knot's 12 x 12 blocks are exact zeros, which add nothing)
 template <int n>
@@ -149,10 +153,21 @@ __device__ __forceinline__ double adm_dot(double init, const double* a, int sa, 
     av[i] = a[sa * i];
     bv[i] = b[i];
   }
-  double acc = init;
+  if constexpr (I7M_ADMM_DOT_CHAINS == 2) {
+    // two interleaved fma chains (even / odd terms) summed at the end: half the dependent latency
+    double a0 = init, a1 = 0.0;
 #pragma unroll
-  for (int i = 0; i < n; ++i) acc += av[i] * bv[i];
-  return acc;
+    for (int i = 0; i < n; i += 2) {
+      a0 += av[i] * bv[i];
+      if (i + 1 < n) a1 += av[i + 1] * bv[i + 1];
+    }
+    return a0 + a1;
+  } else {
+    double acc = init;
+#pragma unroll
+    for (int i = 0; i < n; ++i) acc += av[i] * bv[i];
+    return acc;
+  }
 }
 
 // ... with both operands strided
@@ -648,7 +663,11 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   double* qold = a.sq + (long)b * T;
   double* Pq = a.Pq + (long)b * N * 36;
   double* Pd = a.Pd + (long)b * T;
+#ifdef I7M_DIAG_ADMM_SHARED_REC  // (timing builds only: every problem's iterations read problem 0's stage records)
+  double* Rb = a.R + (long)((PH & 2) ? 0 : b) * (N + 1) * ADM_REC;
+#else
   double* Rb = a.R + (long)b * (N + 1) * ADM_REC;
+#endif
   double* Jb = Rb + REC_J;  // J_k at Jb + ADM_REC k
   double* Ib = a.I + (long)b * m;
   double* qs = a.qs + (long)b * T;

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--chunks", default="0,2048,1024")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--scaling", type=int, default=None, help="OSQP's Ruiz passes (default: the reference's 10)")
+    ap.add_argument("--admm", default=None, help='further OSQP settings as JSON, e.g. \'{"max_iter": 50, "check_termination": 0}\'')
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -33,7 +34,9 @@ def main():
     for rep in range(2):
         for c in [int(x) for x in a.chunks.split(",")]:
             os.environ["I7M_ADMM_CHUNK"] = str(c)
-            kw = {} if a.scaling is None else {"admm": {"scaling": a.scaling}}
+            st = {} if a.scaling is None else {"scaling": a.scaling}
+            st.update(json.loads(a.admm) if a.admm else {})
+            kw = {"admm": st} if st else {}
             h = _lib.Handle(model, N=a.N, max_batch=a.B, qp_mode=_lib.QP_ADMM, **kw)
             xcur, goals, XU = make_batch(h, model, a.B, a.N, seed=45)
             t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
