@@ -59,6 +59,9 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_WPE
 #define I7M_ADMM_WPE 2  // waves per SIMD the adaptive-rho iteration kernel is compiled for
 #endif
+#ifndef I7M_ADMM_SYNC
+#define I7M_ADMM_SYNC 0  // sweep steps' LDS ordering: 0 compiler-only (adm_sweep_sync), 1 wave_sync fences
+#endif
 #ifndef I7M_ADMM_DOT_CHAINS
 #define I7M_ADMM_DOT_CHAINS 2  // fma chains per sweep dot product (adm_dot)
 #endif
@@ -214,6 +217,18 @@ __device__ __forceinline__ double adm_jk(const double* L, double dt, int i, int 
 // coalesced copy of n doubles global -> LDS by the wave
 __device__ __forceinline__ void adm_stage(double* dst, const double* src, int n, int l) {
   for (int e = l; e < n; e += 64) dst[e] = src[e];
+}
+
+// Ordering of one sweep step's LDS traffic between the lanes of its wave.  A wavefront's LDS
+// instructions execute in order, so a lane reads what another lane of the same wave stored by an
+// earlier instruction: only the compiler must keep the order (I7M_ADMM_SYNC 0, an empty asm with a
+// memory clobber).  1: the wave_sync fence, which also waits for every outstanding LDS operation.
+__device__ __forceinline__ void adm_sweep_sync() {
+#if I7M_ADMM_SYNC
+  wave_sync();
+#else
+  __asm__ volatile("" ::: "memory");
+#endif
 }
 
 // OSQP's check_termination on the unscaled residuals (+ the duality gap) and, for adapt_rho,
@@ -728,7 +743,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
     if (lr) sT0[l] = rv * (z[l] - ri * y[l]);
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
-      wave_sync();
+      adm_sweep_sync();
       adm_pf_store(pf, sB, pcode);
       const double xe = fx, qe = fq, ie = fi, t1 = rv * (fz - ri * fy);
       {
@@ -742,7 +757,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
         fy = y[12 * kz + l11];
       }
       if (k < N - 1 && lr) sT1[l] = t1;
-      wave_sync();
+      adm_sweep_sync();
       if (l < nk) {
         const int j = l;
         double acc = j < 12 ? ie * sT0[j] : 0.0;
@@ -751,13 +766,13 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
         if (k > 0 && j < 12) r -= adm_dot<18>(0.0, sC + 18 * j, 1, sW);
         sR[j] = r;
       }
-      wave_sync();
+      adm_sweep_sync();
       double wk = 0.0;
       if (l < nk) {
         wk = adm_dot<18>(0.0, sL + 18 * l, 1, sR);
         wv[18 * k + l] = wk;
       }
-      wave_sync();
+      adm_sweep_sync();
       if (l < nk) sW[l] = wk;
       if (lr) sT0[l] = sT1[l];
     }
@@ -770,7 +785,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
     bw = wv[18 * (N - 1) + l11];
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
-      wave_sync();
+      adm_sweep_sync();
       adm_pf_store(pf, sB, pcode);
       const double we = bw, zr0 = bz, yr0 = by, lr0 = bl, ir0 = bi, xe1 = bx;
       // step k - 1's loads: its blocks, w_{k-1}, block k's rows, x_k (block 0's rows and x_0 at
@@ -785,20 +800,20 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
         bi = Ib[12 * k + l11];
         bx = x[18 * k + (k < N - 1 ? l17 : l11)];
       }
-      wave_sync();
+      adm_sweep_sync();
       if (l < nk) {
         double r = we;
         if (k < N - 1) r -= adm_dot<12>(0.0, sC + l, 18, sW);
         sR[l] = r;
       }
-      wave_sync();
+      adm_sweep_sync();
       double xk = 0.0;
       if (l < nk) xk = adm_dot<18>(0.0, sL + l, 18, sR);
       // sW holds xt_{k+1}'s x part until block k+1's rows are done; sR takes xt_k once every lane
       // has read the right-hand side
-      wave_sync();
+      adm_sweep_sync();
       if (l < nk) sR[l] = xk;
-      wave_sync();
+      adm_sweep_sync();
       if (k < N - 1 && lr) {
         const int r = 12 * (k + 1) + l;
         const double zt = adm_dot<18>(0.0, sJ + 18 * l, 1, sR) + ir0 * sW[l];
@@ -813,7 +828,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
         if (l < nn) x[18 * (k + 1) + l] = al * xtp + (1.0 - al) * xe1;
       }
       xtp = xk;
-      wave_sync();
+      adm_sweep_sync();
       if (lr) sW[l] = sR[l];
     }
     // block 0 rows and x_0 (their old values were loaded at k = 0)
