@@ -35,9 +35,20 @@ __device__ __forceinline__ void lds_sync() {
 // fences of lds_sync() without the s_barrier.  In a single-wave workgroup this is exactly what
 // lds_sync() compiles to; in a multi-wave workgroup (k_sqp_fused) the other waves need not
 // take part.
+//   A wavefront's LDS instructions execute in order, so within one wave only the compiler's order
+// matters: I7M_WAVE_SYNC_FENCE 0 (default) keeps it with an empty asm with a memory clobber; 1 emits
+// the fences, whose s_waitcnt lgkmcnt(0) also drains every outstanding LDS operation.  (No kernel
+// here writes LDS by direct-from-memory loads, whose completion is not ordered with ds_* ops.)
+#ifndef I7M_WAVE_SYNC_FENCE
+#define I7M_WAVE_SYNC_FENCE 0
+#endif
 __device__ __forceinline__ void wave_sync() {
+#if I7M_WAVE_SYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+  __asm__ volatile("" ::: "memory");
+#endif
 }
 // Wave priority (s_setprio 0..3; the SIMD's instruction arbiter otherwise favours the oldest
 // wave).  The Riccati recursion sets it by progress (riccati_mfma_body, BC bit 2: equal-work
