@@ -290,6 +290,16 @@ __device__ __forceinline__ const LsKernArgs* kernarg_ls() {
 // The line search of problem b by the W waves of a workgroup (wave w, lane l): the body of
 // k_linesearch, and the third phase of each SQP iteration of k_sqp_fused.  ls_dyn: the dynamic
 // LDS of ls_lds_bytes(T, W); merit: 9 doubles of LDS.
+// LDS ordering inside the line search: with one wave per problem (W = 1) its LDS instructions
+// execute in order, so a compiler barrier is enough (I7M_LS_WSYNC 1); with W waves, lds_sync.
+#ifndef I7M_LS_WSYNC
+#define I7M_LS_WSYNC 1
+#endif
+template <int W>
+__device__ __forceinline__ void ls_sync() {
+  if constexpr (W == 1 && I7M_LS_WSYNC) __asm__ volatile("" ::: "memory");
+  else lds_sync();
+}
 template <bool SPEC, int ABL = 0, int W = 1, bool FW = false, bool KA = false>
 __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg, const SolveParams& P, const int b,
                                                 const int w, const int l, double* __restrict__ ls_dyn,
@@ -345,7 +355,13 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
   // merit_new equals basemerit bit for bit and alpha = 1 is accepted (src/osqp_sqp.py:58-72).
   // Decided here, not by comparing merits, because the base merit below comes from the
   // linearisation and rounds differently from the candidate evaluation.
-  const bool zero_step = __syncthreads_or(step_nz) == 0;
+  bool zero_step;
+  if constexpr (W == 1 && I7M_LS_WSYNC) {
+    zero_step = __ballot(step_nz) == 0;
+    ls_sync<W>();
+  } else {
+    zero_step = __syncthreads_or(step_nz) == 0;
+  }
   // sum the N knot terms of each candidate slot and store the merit of candidate c0 + slot
   // (c0 already offset by this wave's share of the round; `store` false: compute only)
   double mu_r = P.mu;  // (KA: re-read per round)
@@ -363,7 +379,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
       if (store && k == 0 && slot < R && c0 + slot < 1 + NALPHA) merit[c0 + slot] = o[0] + o[1] + o[2] + mu_r * o[3];
     } else {
       part[l][0] = o[0]; part[l][1] = o[1]; part[l][2] = o[2]; part[l][3] = o[3];
-      lds_sync();
+      ls_sync<W>();
       if (store && l < R && c0 + l < 1 + NALPHA) {
         double qc = 0.0, vc = 0.0, uc = 0.0, cv = 0.0;
         for (int kk = 0; kk < N; ++kk) {
@@ -375,13 +391,13 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
         merit[c0 + l] = qc + vc + uc + mu_r * cv;
       }
     }
-    lds_sync();
+    ls_sync<W>();
   };
   int cstart = 0;
   if (sp.c_begin > 0) {
     // the second launch of a split search: base merit from the first
     if (l == 0 && w == 0) merit[0] = sp.base[b];
-    lds_sync();
+    ls_sync<W>();
     cstart = sp.c_begin;
   } else if (lin && !zero_step) {
     // base merit (src/osqp_sqp.py:52-55) from the linearisation of this XU: |e| (cost[9]) and
@@ -466,7 +482,7 @@ __device__ __forceinline__ void linesearch_body(const DevModel* __restrict__ Mg,
     for (int cc = (c0 == 0 ? 1 : c0); cc < c0 + R * W && cc < c_end; ++cc) {
       if (merit[cc] <= base) { found = cc; break; }
     }
-    lds_sync();
+    ls_sync<W>();
   }
   // (KA: everything below from the kernarg segment, not held across the rounds)
   const LsKernArgs* KE = KA ? kernarg_ls() : nullptr;
