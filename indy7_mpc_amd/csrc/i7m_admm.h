@@ -317,7 +317,8 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
 // column: the -I entry, J's identity / dt entry and 6 linearisation entries; an A row: its -I
 // entry and 18 J entries), so the loads of all of a lane's columns issue together.  The products
 // are the port's (|a_ij| D_j E_i in its order; max is exact), so D, E and c are the one-kernel
-// version's to the bit, the cost sum's wave reduction aside.
+// version's to the bit, the cost sum's wave reduction aside.  Its LDS orderings are fences
+// (wave_sync_fence): as compiler barriers (wave_sync) the kernel ran 0.59 -> 2.42 ms.
 __device__ __forceinline__ double adm_pq(const double* w, int i, int j) { return w[6] * (w[i] * w[j]); }
 template <int CT>
 __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int T, int m, const double* LIN,
@@ -339,7 +340,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 #pragma unroll
   for (int t = 0; t < RT; ++t)
     if (l + 64 * t < m) sE[l + 64 * t] = 1.0;
-  wave_sync();
+  wave_sync_fence();
   double c = 1.0;
   // the P part of column e's inf-norm (knot k, index j in the knot): max_i |P_ij| D_i D_j c
   auto pcol = [&](const double* Cp, int k, int j, double dj) {
@@ -399,7 +400,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       if (blk > 0) mx = fmax(mx, mj);
       etv[t] = 1.0 / sqrt(adm_limit(mx));
     }
-    wave_sync();
+    wave_sync_fence();
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
       const int e = lp + 64 * t;
@@ -410,7 +411,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 #pragma unroll
     for (int t = 0; t < RT; ++t)
       if (lp + 64 * t < m) sE[lp + 64 * t] = sE[lp + 64 * t] * etv[t];
-    wave_sync();
+    wave_sync_fence();
     // cost normalisation: mean column norm of the scaled P, |q|
     double sm = 0.0, qm = 0.0;
 #pragma unroll

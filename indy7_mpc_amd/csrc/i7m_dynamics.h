@@ -42,6 +42,10 @@ __device__ __forceinline__ void lds_sync() {
 #ifndef I7M_WAVE_SYNC_FENCE
 #define I7M_WAVE_SYNC_FENCE 0
 #endif
+__device__ __forceinline__ void wave_sync_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 __device__ __forceinline__ void wave_sync() {
 #if I7M_WAVE_SYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
