@@ -77,7 +77,7 @@ extern "C" {
 /* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
  * layout, field meaning or enum count changes.  4: I7M_QP_ADMM and i7m_config's admm_* fields
  * (appended), I7M_K_COUNT 10 (I7M_K_ADMM, I7M_K_ADMM_PREP), i7m_admm_reset / i7m_get_admm_stats /
- * i7m_get_admm_state (0.4 builds).  3: i7m_config's former `pad` is `h2h_chunks` (a
+ * i7m_get_admm_state, the `precision` field in the former admm_pad slot (0.4 builds).  3: i7m_config's former `pad` is `h2h_chunks` (a
  * nonzero value changes how i7m_solve runs; outside [0, 64] it is refused) and I7M_K_COUNT is 8
  * (I7M_K_LINESEARCH_TAIL added) — size timing arrays from I7M_K_COUNT of this header (0.3 builds).
  * 2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and i7m_set_external_wrench a
@@ -98,6 +98,7 @@ enum { I7M_QP_DIRECT = 0, I7M_QP_BOX = 1, I7M_QP_ADMM = 2 };
  * size (the fused kernel measured slower at every size).  Bit-identical results
  * in every mode. */
 enum { I7M_PIPE_AUTO = 0, I7M_PIPE_SPLIT = 1, I7M_PIPE_FUSED = 2, I7M_PIPE_FUSED_ITER = 3 };
+enum { I7M_PREC_F64 = 0, I7M_PREC_F32 = 1 };
 #define I7M_BOX_Q 1     /* q_lower <= q <= q_upper    description/indy7.urdf:203-238 <limit> */
 #define I7M_BOX_V 2     /* |v| <= velocity limit */
 #define I7M_BOX_U 4     /* |u| <= effort limit */
@@ -151,7 +152,10 @@ typedef struct i7m_config {
   int32_t admm_scaling;         /* Ruiz passes, 10 */
   int32_t admm_check_dualgap;   /* 1: OSQP 1.x's duality-gap test */
   int32_t admm_adaptive_rho_interval; /* 0: never adapt rho; else every this many iterations */
-  int32_t admm_pad;
+  int32_t precision;    /* arithmetic of every kernel (SURVEY.md 8b's ABI sketch): I7M_PREC_F64 (0, the
+                           only one built: the reference's OSQP path computes in double);
+                           I7M_PREC_F32 (GATO's float, gato_controller.py:54-62) is refused by
+                           i7m_create with I7M_EINVAL.  (Was admm_pad: same layout.) */
   double admm_adaptive_rho_tolerance; /* 5 */
 } i7m_config;
 

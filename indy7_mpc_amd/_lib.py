@@ -83,12 +83,13 @@ class i7m_config(C.Structure):
         ("admm_scaling", C.c_int32),
         ("admm_check_dualgap", C.c_int32),
         ("admm_adaptive_rho_interval", C.c_int32),
-        ("admm_pad", C.c_int32),
+        ("precision", C.c_int32),
         ("admm_adaptive_rho_tolerance", C.c_double),
     ]
 
 
 QP_DIRECT, QP_BOX, QP_ADMM = 0, 1, 2
+PREC_F64, PREC_F32 = 0, 1  # i7m_config.precision (only PREC_F64 is built)
 ADMM_RESET_RHO, ADMM_RESET_DUAL, ADMM_RESET_PRIMAL, ADMM_RESET_ALL = 1, 2, 4, 7
 # OSQP's settings as i7m_config_default sets them (oracle/osqp_admm.py DEFAULTS)
 ADMM_DEFAULTS = dict(rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, max_iter=4000, check_termination=25,

@@ -956,6 +956,7 @@ int i7m_config_default(i7m_config* c) {
   c->admm_check_dualgap = 1;
   c->admm_adaptive_rho_interval = 0;
   c->admm_adaptive_rho_tolerance = 5.0;
+  c->precision = I7M_PREC_F64;
   return I7M_OK;
 }
 
@@ -964,6 +965,10 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   *out = nullptr;
   if (cfg->N < 2 || cfg->N > I7M_MAX_N) return fail(I7M_EINVAL, "N must be in [2, 64]");
   if (cfg->max_batch < 1) return fail(I7M_EINVAL, "max_batch must be >= 1");
+  if (cfg->precision != I7M_PREC_F64)
+    return fail(I7M_EINVAL, cfg->precision == I7M_PREC_F32
+                                ? "precision I7M_PREC_F32 is not built: every kernel computes in double (I7M_PREC_F64)"
+                                : "unknown precision");
   if (cfg->max_sqp_iters < 1 || cfg->max_sqp_iters > I7M_MAX_SQP) return fail(I7M_EINVAL, "max_sqp_iters in [1, 8]");
   if (cfg->qp_mode != I7M_QP_DIRECT && cfg->qp_mode != I7M_QP_BOX && cfg->qp_mode != I7M_QP_ADMM)
     return fail(I7M_EINVAL, "unsupported qp_mode");

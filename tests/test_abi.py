@@ -80,6 +80,24 @@ def test_invalid_arguments_are_rejected(lib):
     assert lib.i7m_solve(None, 1, None, None, None, 3, None, None) == -1
 
 
+def test_precision_field_refuses_fp32(lib):
+    """i7m_config.precision (SURVEY.md 8b's ABI sketch): I7M_PREC_F64 is the default and the only
+    arithmetic built; I7M_PREC_F32 (GATO's float, gato_controller.py:54-62) and unknown values are
+    refused by i7m_create before any device work, with a message naming the reason."""
+    from indy7_mpc_amd import _lib
+
+    cfg = _lib.i7m_config()
+    lib.i7m_config_default(C.byref(cfg))
+    assert cfg.precision == _lib.PREC_F64
+    h = C.c_void_p()
+    cfg.precision = _lib.PREC_F32
+    assert lib.i7m_create(C.byref(cfg), C.byref(h)) == -1
+    assert b"I7M_PREC_F32 is not built" in lib.i7m_last_error()
+    cfg.precision = 7
+    assert lib.i7m_create(C.byref(cfg), C.byref(h)) == -1
+    assert b"unknown precision" in lib.i7m_last_error()
+
+
 def test_no_cpu_fallback_without_gpu(lib, model):
     """With no GPU (this container) creating a handle raises — nothing silently runs on CPU."""
     from indy7_mpc_amd import _lib
