@@ -65,6 +65,9 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_DOT_CHAINS
 #define I7M_ADMM_DOT_CHAINS 2  // fma chains per sweep dot product (adm_dot)
 #endif
+#ifndef I7M_ADMM_FSTRIDE
+#define I7M_ADMM_FSTRIDE 19  // the register factor's LDS row stride for S and C (18: 3-way bank conflicts on row reads)
+#endif
 #ifndef I7M_ADMM_FACTOR
 #define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
@@ -485,6 +488,7 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
                            double* Rb, double* sS, double* sJ, double* sL, double* sCp, int l0) {
   const double re = 1e3 * rho, sigma = a.A.sigma;
   const int T = 18 * N - 6;
+  constexpr int FS = I7M_ADMM_FSTRIDE;  // row stride of S and C_{k-1} in LDS
   double* sCol = sL + 324;  // (the sweeps' C slot, free while factoring)
   for (int k = 0; k < N; ++k) {
     const int nk = k < N - 1 ? 18 : 12;
@@ -504,20 +508,20 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
         const double pd = Pd[min(18 * k + i, T - 1)];
         const double ib = Ib[12 * k + ic];
         const double dj = adm_dot2<12>(0.0, sJ + i, 18, sJ + j, 18);
-        const double dc = adm_dot2<18>(0.0, sCp + 18 * ic, 1, sCp + 18 * jc, 1);
+        const double dc = adm_dot2<18>(0.0, sCp + FS * ic, 1, sCp + FS * jc, 1);
         double v = i < 6 && j < 6 ? pq : (i == j && i >= 6 ? pd : 0.0);
         if (i == j) v += sigma;
         if (i == j && i < 12) v += re * (ib * ib);
         if (k < N - 1) v += re * dj;
         if (k > 0 && i < 12 && j < 12) v -= dc;
         if (i >= nk || j >= nk) v = i == j ? 1.0 : 0.0;
-        sS[e] = v;
+        sS[FS * i + j] = v;
       }
     }
     wave_sync();
     double r[18];
 #pragma unroll
-    for (int j = 0; j < 18; ++j) r[j] = sS[18 * lr + j];
+    for (int j = 0; j < 18; ++j) r[j] = sS[FS * lr + j];
 #pragma unroll
     for (int p = 0; p < 18; ++p) {
       const double d = sqrt(adm_readlane(r[p], p));
@@ -535,14 +539,14 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
     wave_sync();  // every lane has read S before L overwrites it
     if (l < 18) {
 #pragma unroll
-      for (int j = 0; j < 18; ++j) sS[18 * l + j] = r[j];
+      for (int j = 0; j < 18; ++j) sS[FS * l + j] = r[j];
     }
     wave_sync();
     double x[18];
 #pragma unroll
     for (int i = 0; i < 18; ++i) {
       // row i of L is read once x_{i-2} exists (two rows of loads in flight, not all 171)
-      int o = 18 * i;
+      int o = FS * i;
       if (i >= 2) asm volatile("" : "+v"(o) : "v"(x[i - 2]));
       double acc = 0.0;
 #pragma unroll
@@ -566,7 +570,7 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
           const int i = e / 18, j = e - 18 * i;
           const double acc = adm_dot2<18>(0.0, sJ + 18 * i, 1, sL + 18 * j, 1);
           const double cv = re * Ib[12 * (k + 1) + i] * acc;
-          sCp[e] = cv;
+          sCp[FS * i + j] = cv;
           Rb[ADM_REC * (k + 1) + REC_C + e] = cv;
         }
       }
@@ -664,7 +668,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
   constexpr bool FAC = (PH & 8) || (PH & 4);
   // (k_admm_prep: sB holds the column scale factors of a Ruiz pass before the factor needs it)
-  __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 324 : 1], sCp[FAC ? 216 : 1], sR[32], sW[32], sT0[16], sT1[16];
+  __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1], sR[32], sW[32], sT0[16], sT1[16];
   __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1];
   double* sL = sB;
   double* sC = sB + 324;
