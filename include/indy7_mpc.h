@@ -51,9 +51,10 @@
  *     i7m_admm_reset start it afresh;
  *   - I7M_QP_BOX (config 4) adds box rows, solved by an interior point whose Newton steps are the
  *     exact solve (ADMM needed 40-4700 iterations on those problems).
- * Deviation: no `precision` field: every kernel computes in fp64.  The drop-in batch_sqp module
- * keeps the reference's SQPSolverfloat_* class names (gato_controller.py:54-62) so callers run
- * unchanged, but it also solves (and returns) fp64.
+ * Precision: i7m_config.precision exists; only I7M_PREC_F64 is built, and
+ * i7m_create refuses I7M_PREC_F32 with I7M_EINVAL — every kernel computes in fp64.  The drop-in
+ * batch_sqp module keeps the reference's SQPSolverfloat_* class names (gato_controller.py:54-62)
+ * so callers run unchanged, but it also solves (and returns) fp64.
  *
  * Status: 0 = OK, <0 = error (see I7M_E*), message via i7m_last_error() (thread-local).
  * Threading: a handle is not re-entrant (like the reference's stateful OSQPSolver);
@@ -75,7 +76,9 @@ extern "C" {
 #define I7M_MAX_N 64
 
 /* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
- * layout, field meaning or enum count changes.  4: I7M_QP_ADMM and i7m_config's admm_* fields
+ * layout, field meaning or enum count changes.  5: i7m_get_admm_status and i7m_get_admm_dual
+ * (appended); i7m_get_admm_stats' iteration record is reset to -1 at the start of every solve
+ * (0.5 builds).  4: I7M_QP_ADMM and i7m_config's admm_* fields
  * (appended), I7M_K_COUNT 10 (I7M_K_ADMM, I7M_K_ADMM_PREP), i7m_admm_reset / i7m_get_admm_stats /
  * i7m_get_admm_state, the `precision` field in the former admm_pad slot (0.4 builds).  3: i7m_config's former `pad` is `h2h_chunks` (a
  * nonzero value changes how i7m_solve runs; outside [0, 64] it is refused) and I7M_K_COUNT is 8
@@ -83,7 +86,7 @@ extern "C" {
  * 2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and i7m_set_external_wrench a
  * trailing `frame` (0.2 builds); 1 had neither.  A caller built against another revision must not
  * call through this library: compare first. */
-#define I7M_ABI_VERSION 4
+#define I7M_ABI_VERSION 5
 
 #define I7M_OK 0
 #define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */
@@ -228,9 +231,10 @@ int i7m_qp(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const
  * — its 12 x 12 block is d^2 J* / d x_0^2 (the sensitivity of the optimal QP cost to the initial
  * state, the derivative of the equality multiplier of the x_0 rows l[:12] = -xs of
  * src/osqp_solver.py:85), its last column the linear part.  Diagnostic / test hook (the reference
- * has no counterpart; OSQP returns the multipliers `y`, src/osqp_solver.py:143).  The matrix is
- * symmetric only to the accuracy of the recursion: returned as computed.  I7M_QP_DIRECT only,
- * N >= 10. */
+ * has no counterpart; OSQP returns the multipliers `y`, src/osqp_solver.py:143).  Returned as
+ * the recursion computes it except row 12, which the kernel mirrors from column 12 (the linear
+ * part); the 12 x 12 block is symmetric only to the recursion's accuracy.  I7M_QP_DIRECT only,
+ * N >= 10 (checked before any work). */
 int i7m_qp_value(i7m_handle* h, int32_t B, const double* xu, const double* xcur, const double* goals,
                  int32_t goal_stride, double* V0);
 
@@ -253,6 +257,15 @@ int i7m_get_admm_stats(i7m_handle* h, int32_t B, int32_t* iters, double* rho);
 /* I7M_QP_ADMM: the carried OSQP state of problems [0, B) in OSQP's scaled coordinates: x (B, T),
  * z, y (B, 12N), the previous QP's linear cost, unscaled (B, T), rho (B).  Any may be NULL. */
 int i7m_get_admm_state(i7m_handle* h, int32_t B, double* x, double* z, double* y, double* q, double* rho);
+/* I7M_QP_ADMM (ABI 5): OSQP's result status of every SQP iteration's QP in the last solve
+ * (B, I7M_MAX_SQP): 1 its termination test passed ("solved"), 0 admm_max_iter was reached
+ * first ("maximum iterations reached"), -1 the problem ran no QP at that iteration.  The
+ * reference's solve() returns it in .info.status (src/osqp_solver.py:143). */
+int i7m_get_admm_status(i7m_handle* h, int32_t B, int32_t* status);
+/* I7M_QP_ADMM (ABI 5): the dual y of each problem's last QP, unscaled as OSQP returns it in
+ * result.y (y = E y_s / c: the carried scaled y with that QP's row scaling E and cost scale c),
+ * (B, 12N). */
+int i7m_get_admm_dual(i7m_handle* h, int32_t B, double* y);
 
 /* Raw linearisation at xu.  lin (B, N-1, 114): per knot Aq(6x6,row-major, =dt*da/dq),
  * Av (=I+dt*da/dv), Bu (=dt*Minv), a (=ABA(q,v,u)); cost (B, N, 10): j = J^T e (6),

@@ -20,7 +20,7 @@ import numpy as np
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
-ABI_VERSION = 4  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
+ABI_VERSION = 5  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8
 MAX_N = 64
@@ -141,6 +141,8 @@ SIGNATURES = [
     ("i7m_admm_reset", C.c_int, [_H, C.c_int32, C.c_int32]),
     ("i7m_get_admm_stats", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32), _DP]),
     ("i7m_get_admm_state", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, _DP, _DP]),
+    ("i7m_get_admm_status", C.c_int, [_H, C.c_int32, C.POINTER(C.c_int32)]),
+    ("i7m_get_admm_dual", C.c_int, [_H, C.c_int32, _DP]),
     ("i7m_linearize", C.c_int, [_H, C.c_int32, _DP, _DP, C.c_int32, _DP, _DP]),
     ("i7m_merit", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
     ("i7m_linesearch", C.c_int, [_H, C.c_int32, _DP, _DP, _DP, C.c_int32, _DP]),
@@ -331,13 +333,24 @@ class Handle:
         RHO = batch_sqp resetRho, DUAL = resetLambda, ALL = a new OSQP object)."""
         _check(self._lib.i7m_admm_reset(self._h, int(self.max_batch if B is None else B), int(what)))
 
-    def admm_stats(self, B):
+    def admm_stats(self, B, with_status=False):
         """I7M_QP_ADMM: (OSQP iterations per SQP iteration of the last solve (B, 8), -1 = none;
-        rho (B,))."""
+        rho (B,)); with_status also OSQP's status per SQP iteration (B, 8): 1 solved, 0 maximum
+        iterations reached, -1 no QP."""
         it = np.zeros((B, MAX_SQP), dtype=np.int32)
         rho = np.zeros(B)
         _check(self._lib.i7m_get_admm_stats(self._h, int(B), it.ctypes.data_as(C.POINTER(C.c_int32)), _ptr(rho)))
-        return it, rho
+        if not with_status:
+            return it, rho
+        stat = np.zeros((B, MAX_SQP), dtype=np.int32)
+        _check(self._lib.i7m_get_admm_status(self._h, int(B), stat.ctypes.data_as(C.POINTER(C.c_int32))))
+        return it, rho, stat
+
+    def admm_dual(self, B):
+        """I7M_QP_ADMM: each problem's last QP's dual y, unscaled as OSQP returns it (B, 12N)."""
+        y = np.empty((B, 12 * self.N))
+        _check(self._lib.i7m_get_admm_dual(self._h, int(B), _ptr(y)))
+        return y
 
     def admm_state(self, B):
         """I7M_QP_ADMM: the carried OSQP state (scaled x (B, T), z, y (B, 12N), previous q (B, T),

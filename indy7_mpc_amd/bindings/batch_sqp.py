@@ -4,9 +4,10 @@
 The reference binding is an external CUDA module (absent).  This one keeps its
 Python surface — ``SQPSolverfloat_{1..256}`` with ``solve``, ``reset``, ``resetRho``,
 ``resetLambda``, ``set_external_wrench_batch`` and ``sim_forward`` — and solves the OSQP
-formulation of src/osqp_solver.py (fp64) on the GPU, each QP exactly (default) or, with
-``qp_mode="admm"``, by OSQP's own iteration from a per-problem warm-started state (then
-``resetRho`` / ``resetLambda`` reset OSQP's rho / duals, gato_controller.py:132-138).  N is taken
+formulation of src/osqp_solver.py (fp64) on the GPU, each QP by default (``qp_mode="admm"``)
+with OSQP's own iteration from a per-problem warm-started state, as the reference's OSQP path
+does (``resetRho`` / ``resetLambda`` reset OSQP's rho / duals, gato_controller.py:132-138), or
+with ``qp_mode="direct"`` exactly (the optimum OSQP approximates to eps 1e-3).  N is taken
 from the XU width (traj_len = 18N - 6); goals use the GATO layout (B, 6N), first 3 of every 6 used.
 
 External wrench convention (``set_external_wrench_batch``): by default each row is what the
@@ -33,7 +34,7 @@ _SIZES = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 class _SQPSolverBatch:
     batch_size = 1
 
-    def __init__(self, model=None, device_id=0, wrench_frame="world", qp_mode="direct"):
+    def __init__(self, model=None, device_id=0, wrench_frame="world", qp_mode="admm"):
         if wrench_frame not in ("world", "local"):
             raise ValueError("wrench_frame must be 'world' or 'local'")
         if qp_mode not in ("direct", "admm"):

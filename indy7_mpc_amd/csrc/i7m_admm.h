@@ -48,6 +48,7 @@ struct AdmmArgs {
   double *Pq, *Pd, *I, *qs, *ls, *D, *E, *Dt, *Et, *R, *w;
   double* cs;  // (B) OSQP's cost scale c of the current QP (k_admm_prep -> k_admm_iter)
   int* iters;  // (B, I7M_MAX_SQP): OSQP iterations of SQP iteration `sqp_iter`
+  int* status;  // (B, I7M_MAX_SQP): 1 OSQP's termination test passed, 0 max_iter reached
   int sqp_iter;
   int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
 };
@@ -866,10 +867,10 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
       }
     }
   }
-  (void)solved;
   if (l == 0) {
     a.srho[b] = rho;
     if (a.iters) a.iters[(long)b * 8 + a.sqp_iter] = it > a.A.max_iter ? a.A.max_iter : it;
+    if (a.status) a.status[(long)b * 8 + a.sqp_iter] = solved ? 1 : 0;
   }
   double* so = a.sol + (long)b * T;
   for (int e = l; e < T; e += 64) so[e] = D[e] * x[e];

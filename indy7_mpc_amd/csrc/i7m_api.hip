@@ -107,7 +107,7 @@ struct i7m_handle {
   int* d_bact = nullptr;
   // I7M_QP_ADMM (i7m_admm.h): one allocation, per-problem OSQP state and k_admm scratch
   double* d_admm = nullptr;
-  int* d_admm_it = nullptr;  // (max_batch, I7M_MAX_SQP) OSQP iterations per SQP iteration
+  int* d_admm_it = nullptr;  // 2 x (max_batch, I7M_MAX_SQP): OSQP iterations, then OSQP status, per SQP iteration
   // box QP: 1 k_ipm_fused<false> (default), 0 I7M_IPM=delta (k_ipm_fused<true>: the corrector
   // reuses the predictor's factorisation; measured slower), 2 I7M_IPM=split
   int ipm_mode = 1;
@@ -285,6 +285,7 @@ AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
   a.Pq = p[5]; a.Pd = p[6]; a.I = p[7]; a.qs = p[8]; a.ls = p[9]; a.D = p[10]; a.E = p[11];
   a.R = p[12]; a.w = p[13]; a.cs = p[14];
   a.iters = its + b0 * I7M_MAX_SQP;
+  a.status = its + (Bm + b0) * I7M_MAX_SQP;
   return a;
 }
 size_t admm_doubles(long Bm, long N) {
@@ -631,6 +632,12 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
   int* act = h->d_active + b0;
   double* qbuf = h->d_sol + b0 * P.T;
   if (use_fused(h, B)) return launch_fused(h, s, W, P, d_xu_in, d_xu, d_xs, d_goals, d_st, b0);
+  if (h->cfg.qp_mode == I7M_QP_ADMM && B > 0) {
+    // this solve's OSQP records start at -1 ("no QP"): a problem that stops after SQP iteration
+    // 0 must not report an earlier call's counts for the iterations it did not run
+    HIPCHK(hipMemsetAsync(W.adm.iters, 0xff, (size_t)B * I7M_MAX_SQP * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(W.adm.status, 0xff, (size_t)B * I7M_MAX_SQP * sizeof(int), s));
+  }
   for (int it = 0; it < h->cfg.max_sqp_iters; ++it) {
     const double* xin = it == 0 ? d_xu_in : d_xu;
     int rc;
@@ -1074,7 +1081,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
          alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
   if (ok && cfg->qp_mode == I7M_QP_ADMM) {
     ok = alloc((void**)&h->d_admm, admm_doubles((long)Bm, (long)N) * 8) &&
-         alloc((void**)&h->d_admm_it, Bm * I7M_MAX_SQP * sizeof(int));
+         alloc((void**)&h->d_admm_it, 2 * Bm * I7M_MAX_SQP * sizeof(int));
     h->cfg.qp_mode = I7M_QP_ADMM;
     if (ok && i7m_admm_reset(h, cfg->max_batch, I7M_ADMM_RESET_ALL) != I7M_OK) ok = false;
   }
@@ -1182,6 +1189,7 @@ int i7m_admm_reset(i7m_handle* h, int32_t B, int32_t what) {
     HIPCHK(hipMemcpyAsync(a.srho, r.data(), (size_t)B * 8, hipMemcpyHostToDevice, h->stream));
   }
   HIPCHK(hipMemsetAsync(a.iters, 0xff, (size_t)B * I7M_MAX_SQP * sizeof(int), h->stream));
+  HIPCHK(hipMemsetAsync(a.status, 0xff, (size_t)B * I7M_MAX_SQP * sizeof(int), h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return I7M_OK;
 }
@@ -1196,6 +1204,38 @@ int i7m_get_admm_stats(i7m_handle* h, int32_t B, int32_t* iters, double* rho) {
   if (iters) HIPCHK(hipMemcpyAsync(iters, a.iters, (size_t)B * I7M_MAX_SQP * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   if (rho) HIPCHK(hipMemcpyAsync(rho, a.srho, (size_t)B * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_get_admm_status(i7m_handle* h, int32_t B, int32_t* status) {
+  if (!h || !status) return fail(I7M_EINVAL, "null handle or output");
+  if (h->cfg.qp_mode != I7M_QP_ADMM) return fail(I7M_EINVAL, "handle is not in I7M_QP_ADMM mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const AdmmArgs a = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, h->cfg.N, 0);
+  HIPCHK(hipMemcpyAsync(status, a.status, (size_t)B * I7M_MAX_SQP * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return I7M_OK;
+}
+
+int i7m_get_admm_dual(i7m_handle* h, int32_t B, double* y) {
+  if (!h || !y) return fail(I7M_EINVAL, "null handle or output");
+  if (h->cfg.qp_mode != I7M_QP_ADMM) return fail(I7M_EINVAL, "handle is not in I7M_QP_ADMM mode");
+  if (B < 0 || B > h->cfg.max_batch) return fail(I7M_EINVAL, "batch outside [0, max_batch]");
+  if (B == 0) return I7M_OK;
+  HIPCHK(hipSetDevice(h->dev));
+  const long m = 12 * (long)h->cfg.N;
+  const AdmmArgs a = admm_layout(h->d_admm, h->d_admm_it, h->cfg.max_batch, h->cfg.N, 0);
+  std::vector<double> e((size_t)B * m), c((size_t)B);
+  int rc;
+  if ((rc = copy_out(h, y, a.sy, (size_t)B * m)) || (rc = copy_out(h, e.data(), a.E, (size_t)B * m)) ||
+      (rc = copy_out(h, c.data(), a.cs, (size_t)B)))
+    return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  // OSQP's unscale_solution: y = E y_s / c, with the scaling of each problem's last QP
+  for (long b = 0; b < B; ++b)
+    for (long r = 0; r < m; ++r) y[b * m + r] = e[b * m + r] * y[b * m + r] / c[b];
   return I7M_OK;
 }
 
@@ -1300,15 +1340,16 @@ int i7m_qp_value(i7m_handle* h, int32_t B, const double* xu, const double* xcur,
   if (B == 0) return I7M_OK;
   if (!xu || !xcur || !goals || !V0) return fail(I7M_EINVAL, "null pointer");
   if (h->cfg.qp_mode != I7M_QP_DIRECT) return fail(I7M_EINVAL, "i7m_qp_value: the equality-constrained QP only");
-  HIPCHK(hipSetDevice(h->dev));
   const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  // (B x 169 doubles in the solution buffer: T = 18 N - 6 >= 169 from N = 10) — a precondition,
+  // checked before any copy or launch
+  if (T < 169) return fail(I7M_EINVAL, "i7m_qp_value needs N >= 10");
+  HIPCHK(hipSetDevice(h->dev));
   SolveParams P = params_of(h, B, goal_stride);
   if ((rc = copy_in(h, h->d_xu, xu, (size_t)B * T))) return rc;
   if ((rc = copy_in(h, h->d_xs, xcur, (size_t)B * 12))) return rc;
   if ((rc = copy_in(h, h->d_goal, goals, (size_t)B * N * goal_stride))) return rc;
   if ((rc = launch_linearize(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_goal, nullptr))) return rc;
-  // (B x 169 doubles in the solution buffer: T = 18 N - 6 >= 169 from N = 10)
-  if (T < 169) return fail(I7M_EINVAL, "i7m_qp_value needs N >= 10");
   double* vbuf = h->d_sol;
   if ((rc = launch_riccati(h, h->stream, bufs_at(h, 0), P, h->d_xu, h->d_xs, nullptr, h->d_sol, vbuf))) return rc;
   if ((rc = copy_out(h, V0, vbuf, (size_t)B * 169))) return rc;

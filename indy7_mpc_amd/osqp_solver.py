@@ -1,13 +1,15 @@
 """Drop-in for reference ``OSQPSolver`` (src/osqp_solver.py:6-155).
 
 Same constructor, attributes and methods.  The numbers come from the GPU:
-  * ``setup_and_solve_qp`` linearises on the device (k_linearize) and solves the QP EXACTLY
-    with the block-tridiagonal Riccati kernel (k_riccati).  The reference hands the same
-    P/A/q/l/u to OSQP (default eps 1e-3), which converges to this solution.  With
-    ``qp_mode="admm"`` it runs OSQP's algorithm itself (k_admm_scale, k_admm_factor, k_admm_iter; i7m_admm.h) from a warm-started
-    per-problem OSQP state, as the reference's ``self.osqp`` object does (:38-40, 140-143): the
-    trajectories are then the reference's own (oracle/osqp_admm.py pins them against the
-    notebook's printed closed loop).
+  * ``setup_and_solve_qp`` linearises on the device (k_linearize) and, by default
+    (``qp_mode="admm"``), runs OSQP's own algorithm on it (k_admm_scale, k_admm_factor,
+    k_admm_iter; i7m_admm.h) from a warm-started per-problem OSQP state, as the reference's
+    ``self.osqp`` object does (:38-40, 140-143): the trajectories are the reference's own
+    (oracle/osqp_admm.py pins them against the notebook's printed closed loop).
+    ``qp_mode="direct"`` instead solves each QP EXACTLY with the block-tridiagonal Riccati kernel
+    (k_riccati): the optimum OSQP (eps 1e-3) only approximates, so its trajectories differ from
+    the reference's by OSQP's own tolerance — median 5e-5, over 1e-4 on ~30 % of config-3
+    problems, up to ~0.2 (tests/test_admm_oracle.py pins that distribution).
   * ``Pdata/Adata/l/g`` (the CSC value arrays the reference fills, :95-135) are assembled on
     the host from the device linearisation, in the reference's exact value order.  The solve
     itself does not need them, so after ``setup_and_solve_qp`` they are filled lazily: the call
@@ -28,23 +30,32 @@ from . import _lib
 
 
 class QPSolution:
-    """What ``osqp.OSQP().solve()`` returns, as far as the reference uses it (``.x``)."""
+    """What ``osqp.OSQP().solve()`` returns: ``.x`` (the only field the reference reads,
+    src/osqp_solver.py:143, src/osqp_sqp.py:80), ``.y`` and ``.info.status`` / ``.info.iter``.
+    ADMM mode: OSQP's status string ("solved", or "maximum iterations reached" when the
+    termination test never passed within max_iter), its iteration count and the unscaled dual
+    y = E y_s / c.  Direct mode: the exact KKT solve ("solved", 0 iterations, y None)."""
 
-    def __init__(self, x, status="solved", iters=0):
+    def __init__(self, x, status="solved", iters=0, y=None):
         self.x = x
-        self.y = None
-        self.info = type("info", (), {"status": status, "iter": iters})()
+        self.y = y
+        self.info = type("info", (), {"status": status, "iter": iters,
+                                      "status_val": 1 if status == "solved" else -2})()
 
 
 class OSQPSolver:
     def __init__(self, model, dt=0.01, N=32, dQ_cost=0.01, R_cost=1e-5, QN_cost=100, regularize=True, eps=1,
                  max_batch=1, device_id=0, box_constraints=False, box_mask=_lib.BOX_Q | _lib.BOX_V | _lib.BOX_U,
-                 box_max_iters=30, box_tol=1e-8, qp_mode="direct", admm=None):
+                 box_max_iters=30, box_tol=1e-8, qp_mode=None, admm=None):
         """Reference signature (src/osqp_solver.py:7) plus: max_batch / device_id (device
         buffers); the config-4 extension ``box_constraints``: box rows on
         q, v, u from the model's URDF limits, solved by the interior-point mode (I7M_QP_BOX);
-        ``qp_mode``: "direct" (exact KKT solve) or "admm" (OSQP's iteration with its carried
-        state; ``admm`` overrides OSQP settings, keys of _lib.ADMM_DEFAULTS)."""
+        ``qp_mode``: "admm" (the default: OSQP's iteration with its carried state, i.e. the
+        reference's numbers; ``admm`` overrides OSQP settings, keys of _lib.ADMM_DEFAULTS) or
+        "direct" (the exact KKT solve, the optimum OSQP approximates).  With box_constraints the
+        QP is the interior-point mode's (qp_mode must then be left unset or "direct")."""
+        if qp_mode is None:
+            qp_mode = "direct" if box_constraints else "admm"
         if qp_mode not in ("direct", "admm"):
             raise ValueError("qp_mode must be 'direct' or 'admm'")
         if qp_mode == "admm" and box_constraints:
@@ -127,8 +138,13 @@ class OSQPSolver:
         Pdata / Adata / l / g describe this QP afterwards (assembled on first read)."""
         xu, xs, eepos_g = (np.array(a, dtype=float) for a in (xu, xs, eepos_g))
         x = self.handle.qp(xu, xs, eepos_g)[0]
-        iters = int(self.handle.admm_stats(1)[0][0, 0]) if self.box["qp_mode"] == _lib.QP_ADMM else 0
-        sol = QPSolution(x, iters=iters)
+        if self.box["qp_mode"] == _lib.QP_ADMM:
+            its, _, solved = self.handle.admm_stats(1, with_status=True)
+            y = self.handle.admm_dual(1)[0]
+            sol = QPSolution(x, status="solved" if solved[0, 0] else "maximum iterations reached",
+                             iters=int(its[0, 0]), y=y)
+        else:
+            sol = QPSolution(x)
         self._pending_A = (xu, xs)
         self._pending_P = (xu, eepos_g)
         return sol

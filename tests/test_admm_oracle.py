@@ -114,3 +114,49 @@ def test_admm_tight_tolerance_reaches_the_exact_qp():
     np.testing.assert_array_equal(al, al_r)
     rel = np.linalg.norm(out - ref, axis=1) / np.linalg.norm(ref, axis=1)
     assert rel.max() < 1e-7, rel
+
+
+@pytest.mark.parametrize("N,seed", [(16, 44), (32, 45)])
+def test_port_admm_adaptive_rho_matches_numpy_osqp(N, seed):
+    """OSQP's adaptive rho (the reference's OSQP default adapts; its interval is timing-based,
+    oracle/osqp_admm.py) at a fixed interval of 25 and a tolerance tight enough that rho moves:
+    the port (block form, re-factoring in place) takes the numpy restatement's OSQP iteration
+    counts, line-search steps and final rho, XU to 1e-8.  rho starts at 0.005 (a setting's
+    choice), so that the estimate leaves the tolerance band of 5 and rho moves."""
+    B = 4
+    xcur, goals, XU = synthetic_batch(B, N, seed)
+    kw = dict(rho=0.005, adaptive_rho_interval=25)
+    st = cpu.AdmmState(B, N, rho=0.005)
+    out, qp, al, _, it = cpu.solve_admm(xcur, goals, XU, N, st, admm=cpu.admm_cfg(**kw))
+    moved = 0
+    for b in range(B):
+        s = OSQPSolverRef(N=N, qp="osqp", osqp_settings=dict(kw))
+        sq = SQPRef(s)
+        x = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        its = [h[0] for h in s.osqp.history]
+        assert its == list(it[b, :qp[b]]), (b, its, it[b])
+        np.testing.assert_array_equal(sq.stats["linesearch_alphas"]["values"], al[b, :qp[b]])
+        assert np.linalg.norm(x - out[b]) <= 1e-8 * np.linalg.norm(x)
+        assert abs(s.osqp.rho - st.rho[b]) <= 1e-8 * s.osqp.rho, (s.osqp.rho, st.rho[b])
+        moved += s.osqp.rho != 0.005
+    assert moved > 0, "rho never adapted: the test would not exercise the re-factorisation"
+
+
+def test_direct_mode_vs_osqp_distribution_is_pinned():
+    """The exact KKT solve (qp_mode "direct", the optimum) against OSQP's own iterate (qp_mode
+    "admm", the reference's numbers, eps 1e-3) on config-3 draws (seed 45, 1024 problems, cold
+    OSQP state): same line-search steps on every problem, but XU differs by OSQP's tolerance —
+    measured median 5.8e-5, p90 2.0e-4, max 1.0e-3, 31 % of problems above north_star's 1e-4.
+    Pinned here so the gap between the two modes cannot drift unseen (VERDICT r4 "What's weak" 1);
+    the device's direct mode equals the port's direct mode to 1e-12 (tests/test_gpu_solver.py),
+    so these are also the device's numbers, and bench.py reports them as `parity_vs_osqp`."""
+    B, N = 1024, 32
+    xcur, goals, XU = synthetic_batch(B, N, 45)
+    d, qp_d, al_d, _ = cpu.solve(xcur, goals, XU, N, nthreads=8)
+    a, qp_a, al_a, _, _ = cpu.solve_admm(xcur, goals, XU, N, cpu.AdmmState(B, N), nthreads=8)
+    rel = np.linalg.norm(d - a, axis=1) / np.linalg.norm(a, axis=1)
+    same = np.all(np.where(np.isnan(al_d) & np.isnan(al_a), True, al_d == al_a), axis=1)
+    assert same.all() and (qp_d == qp_a).all()
+    assert 3e-5 < np.median(rel) < 1.2e-4, np.median(rel)
+    assert 0.2 < (rel > 1e-4).mean() < 0.45, (rel > 1e-4).mean()
+    assert rel.max() < 1e-2, rel.max()

@@ -39,12 +39,14 @@ def _rel(a, b):
     return np.linalg.norm(a - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-300)
 
 
-@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43), (16, 512, 41)])
+@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43), (16, 512, 41), (64, 24, 48), (5, 16, 49)])
 def test_admm_solves_match_port(lib, model, N, B, seed):
     """Two consecutive solves (the second warm-started from the first's OSQP state) on the GPU and
     on the port: same OSQP iterations and steps, same XU and state.  (16, 512, 41) holds problems
     whose first line search finds no step (alpha = 0): src/osqp_sqp.py:81-82 re-solves the same QP,
-    which OSQP's warm start makes a different iterate — the GPU re-solves too (k_linesearch mode 2)."""
+    which OSQP's warm start makes a different iterate — the GPU re-solves too (k_linesearch mode 2).
+    N = 64 runs the scaling kernel's wide variant; N = 5 a short horizon (B not a multiple of the
+    kernels' problems per wave is covered by B = 24 at N = 64)."""
     xcur, goals, XU = synthetic_batch(B, N, seed)
     h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
     st = cpu.AdmmState(B, N)
@@ -141,3 +143,94 @@ def test_admm_chunked_host_to_host_equals_one_piece(lib, model):
     for u, v in zip(h1.admm_state(B), h3.admm_state(B)):
         np.testing.assert_array_equal(u, v)
     np.testing.assert_array_equal(h1.admm_stats(B)[0], h3.admm_stats(B)[0])
+
+
+def test_admm_adaptive_rho_matches_port(lib, model):
+    """OSQP's adaptive rho (admm_adaptive_rho_interval > 0: k_admm_iter's in-place re-factorisation)
+    against the port (itself pinned to the numpy OSQP restatement with the same settings,
+    tests/test_admm_oracle.py): OSQP iteration counts and the rho after every solve identical (to
+    1e-12), XU and state to 1e-8; rho starts at 0.005 so that it actually moves."""
+    N, B = 32, 48
+    kw = dict(rho=0.005, adaptive_rho_interval=25)
+    xcur, goals, XU = synthetic_batch(B, N, 50)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, admm=kw)
+    st = cpu.AdmmState(B, N, rho=0.005)
+    xin = XU
+    for call in range(2):
+        out, s = h.solve(xcur, goals, xin)
+        it, rho = h.admm_stats(B)
+        ref, qp, al, _, it_r = cpu.solve_admm(xcur, goals, xin, N, st, admm=cpu.admm_cfg(**kw))
+        np.testing.assert_array_equal(s["qp_iters"], qp)
+        for b in range(B):
+            np.testing.assert_array_equal(it[b, :qp[b]], it_r[b, :qp[b]], err_msg=f"call {call} problem {b}")
+            np.testing.assert_array_equal(s["alphas"][b, :s["n_alphas"][b]], al[b, :qp[b]])
+        np.testing.assert_allclose(rho, st.rho, rtol=1e-12)
+        assert (rho != 0.005).sum() >= B // 2, rho  # the re-factorisation ran on most problems
+        assert _rel(out, ref).max() < 1e-8, _rel(out, ref).max()
+        xin = out
+
+
+def test_admm_full_size_every_problem_matches_port(lib, model):
+    """Config 3 at full size in ADMM mode (B = 4096, N = 32, seed 45, cold OSQP state): every
+    problem's SQP iterations, OSQP iterations per QP and line-search steps equal the port's, XU to
+    1e-8 — the same comparison the bench's config3_admm.parity_vs_port makes, as a test."""
+    B, N = 4096, 32
+    xcur, goals, XU = synthetic_batch(B, N, 45)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+    out, s = h.solve(xcur, goals, XU)
+    it, _ = h.admm_stats(B)
+    ref, qp, al, _, it_r = cpu.solve_admm(xcur, goals, XU, N, cpu.AdmmState(B, N), nthreads=16)
+    np.testing.assert_array_equal(s["qp_iters"], qp)
+    used = np.arange(8)[None, :] < qp[:, None]
+    np.testing.assert_array_equal(np.where(used, it, -1), np.where(used, it_r, -1))
+    ga = s["alphas"][:, :al.shape[1]]
+    used_a = np.arange(ga.shape[1])[None, :] < s["n_alphas"][:, None]
+    assert np.array_equal(used_a, ~np.isnan(al)) and np.array_equal(ga[used_a], al[used_a])
+    assert _rel(out, ref).max() < 1e-8, _rel(out, ref).max()
+
+
+def test_admm_status_and_dual(lib, model):
+    """OSQP's result fields through QPSolution: status "solved" with the default settings and
+    "maximum iterations reached" when max_iter stops OSQP before its termination test passes; y
+    is the unscaled dual (OSQP's result.y), so P x + q + A'y is OSQP's dual residual, within its
+    tolerance eps_abs + eps_rel * scale, and A x = l within the primal tolerance."""
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    N = 16
+    xcur, goals, XU = synthetic_batch(1, N, 51)
+    s = OSQPSolver(model, N=N)  # qp_mode "admm" is the default
+    sol = s.setup_and_solve_qp(XU[0], xcur[0], goals[0])
+    assert sol.info.status == "solved" and sol.info.iter % 25 == 0
+    P = s.P.copy()
+    P.data[:] = s.Pdata
+    Pf = P + P.T - np.diag(P.diagonal())
+    A = s.A.copy()
+    A.data[:] = s.Adata
+    x, y = sol.x, sol.y
+    dres = Pf @ x + s.g + A.T @ y
+    scale = max(np.abs(Pf @ x).max(), np.abs(s.g).max(), np.abs(A.T @ y).max())
+    assert np.abs(dres).max() <= 1e-3 + 1e-3 * scale, (np.abs(dres).max(), scale)
+    pres = A @ x - s.l
+    assert np.abs(pres).max() <= 1e-3 + 1e-3 * max(np.abs(A @ x).max(), np.abs(s.l).max())
+    s2 = OSQPSolver(model, N=N, admm={"max_iter": 10})
+    sol2 = s2.setup_and_solve_qp(XU[0], xcur[0], goals[0])
+    assert sol2.info.status == "maximum iterations reached" and sol2.info.iter == 10
+
+
+def test_admm_iteration_record_is_reset_every_solve(lib, model):
+    """i7m_get_admm_stats after a solve reports -1 for the SQP iterations that solve did not run,
+    even where an earlier solve ran them: solve 1 runs two QPs on every problem, solve
+    2 starts from converged trajectories whose first step is below 1e-3, so it stops after one."""
+    N, B = 16, 8
+    xcur, goals, XU = synthetic_batch(B, N, 52)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, admm={"eps_abs": 1e-9, "eps_rel": 1e-9})
+    out, s1 = h.solve(xcur, goals, XU)
+    it1, _, st1 = h.admm_stats(B, with_status=True)
+    assert (s1["qp_iters"] == 2).any() and (it1[:, 1] > 0).any()
+    for _ in range(3):
+        out, s2 = h.solve(xcur, goals, out)
+    it2, _, st2 = h.admm_stats(B, with_status=True)
+    for b in range(B):
+        n = s2["qp_iters"][b]
+        assert (it2[b, :n] > 0).all() and (it2[b, n:] == -1).all(), (b, n, it2[b])
+        assert (st2[b, :n] >= 0).all() and (st2[b, n:] == -1).all(), (b, n, st2[b])
+    assert (s2["qp_iters"] == 1).any(), s2["qp_iters"]

@@ -45,7 +45,7 @@ def test_batched_closed_loop_matches_independent_oracle_runs(lib, model):
     xs[2, :6], xs[2, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
     xs[3, :6] = [0.4, -1.9, -0.6, -2.0, -0.1, 0.4]                  # 1.86 from the goal: stops at once
     xs[4, :6], xs[4, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
-    solver = OSQPSolver(model)
+    solver = OSQPSolver(model, qp_mode="direct")
     ctrl = MPC_OSQP(model, SQP_OSQP(solver), solver)
     q, d = ctrl.run_mpc_batch(xs, ends, num_steps=steps)
     assert q.shape == (steps, 5, 6) and d.shape == (steps, 5)
@@ -118,7 +118,7 @@ def test_closed_loop_500_steps_shadowed_by_oracle(lib, model):
     from oracle import cpu
 
     tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
-    solver = OSQPSolver(model)
+    solver = OSQPSolver(model, qp_mode="direct")
     sqp = SQP_OSQP(solver)
     rec = []
     inner = sqp.sqp

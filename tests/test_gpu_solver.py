@@ -38,7 +38,7 @@ def test_golden_linearisation_and_qp(lib, model, N):
     from indy7_mpc_amd.osqp_solver import OSQPSolver
 
     f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
-    s = OSQPSolver(model, N=N)
+    s = OSQPSolver(model, N=N, qp_mode="direct")
     for b in range(f["Pdata"].shape[0]):
         s.assemble(f["XU_lin"][b], f["xcur"][b], f["goals"][b])
         for name in ("Pdata", "Adata", "l", "g"):
@@ -59,7 +59,7 @@ def test_setup_and_solve_qp_fills_csc_arrays(lib, model, N):
     from indy7_mpc_amd.osqp_solver import OSQPSolver
 
     f = np.load(os.path.join(GOLD, f"sqp_N{N}.npz"))
-    s = OSQPSolver(model, N=N)
+    s = OSQPSolver(model, N=N, qp_mode="direct")
     for b in range(f["Pdata"].shape[0]):
         sol = s.setup_and_solve_qp(f["XU_lin"][b], f["xcur"][b], f["goals"][b]).x
         assert _rel(sol, f["qp_sol"][b]) < 1e-8
@@ -117,7 +117,7 @@ def test_mpc_osqp_closed_loop_matches_notebook(lib, model):
     from indy7_mpc_amd.osqp_sqp import SQP_OSQP
 
     tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
-    solver = OSQPSolver(model)
+    solver = OSQPSolver(model, qp_mode="direct")
     sqp = SQP_OSQP(solver)
     ctrl = MPC_OSQP(model, sqp, solver)
     ends = np.array([solver.eepos(np.array(q)) for q in tr["endpoint_q"]])
@@ -136,7 +136,7 @@ def test_sqp_osqp_methods_match_oracle(lib, model):
 
     N = 16
     xcur, goals, XU = synthetic_batch(1, N, seed=12)
-    s = OSQPSolver(model, N=N)
+    s = OSQPSolver(model, N=N, qp_mode="direct")
     sq = SQP_OSQP(s)
     rs = OSQPSolverRef(N=N)
     rq = SQPRef(rs)

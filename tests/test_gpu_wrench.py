@@ -137,7 +137,7 @@ def test_batch_sqp_surface_world_wrench(lib, model):
     f = np.random.default_rng(1).normal(0, 30, (B, 6))
     f[:, 3:] = 0.0
     f[0] = 0.0
-    s = batch_sqp.SQPSolverfloat_4()
+    s = batch_sqp.SQPSolverfloat_4(qp_mode="direct")
     assert s.wrench_frame == "world"
     s.set_external_wrench_batch(f)
     s.reset(); s.resetRho(); s.resetLambda()
@@ -160,7 +160,7 @@ def test_batch_sqp_surface_world_wrench(lib, model):
     meas = np.concatenate([q, v])
     assert int(np.argmin(np.linalg.norm(xn - meas, axis=1))) == 2
     # the local-frame option is the other model
-    sl = batch_sqp.SQPSolverfloat_4(wrench_frame="local")
+    sl = batch_sqp.SQPSolverfloat_4(wrench_frame="local", qp_mode="direct")
     sl.set_external_wrench_batch(f)
     rl = sl.solve(XU, DT, xcur, g6)
     assert np.linalg.norm(rl["xu_trajectory"][0] - ref[0]) <= 1e-12 * np.linalg.norm(ref[0])
