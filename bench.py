@@ -267,10 +267,10 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
 
 def admm_bytes_per_iter(N: int):
     """HBM bytes one OSQP iteration of k_admm_iter streams per problem (i7m_admm.h): the forward and the
-    backward sweep each read every stage's packed Linv (171), coupling C (216) and compact scaled J
-    (120) doubles, plus the per-knot vectors (x, q, z, y, w, xt and the scaling rows: ~120 doubles
-    per knot)."""
-    return 8 * (2 * (171 * N + 336 * (N - 1)) + 120 * N)
+    backward sweep each read every stage's record (ADM_REC = 292 doubles: packed Linv_k 171, compact
+    scaled J_k 120, one pad; the coupling block is never stored), plus the per-knot vectors (x, q, z,
+    y, w, the scaling rows: ~120 doubles per knot)."""
+    return 8 * (2 * 292 * N + 120 * N)
 
 
 def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 32, native=None,

@@ -51,6 +51,7 @@ struct AdmmArgs {
   int* status;  // (B, I7M_MAX_SQP): 1 OSQP's termination test passed, 0 max_iter reached
   int sqp_iter;
   int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
+  int ablate;  // I7M_DIAG builds only (I7M_ABLATE, timing variants, results invalid); 0 otherwise
 };
 
 // HBM layout of the per-stage blocks (what every OSQP iteration streams): the inverted diagonal
@@ -82,12 +83,11 @@ struct AdmmArgs {
 #define I7M_ADMM_ITER_WPE 2  // ... and k_admm_iter without adaptive rho (at 3: 78 spilled VGPRs, 30% slower)
 #endif
 constexpr int ADM_LP = 171, ADM_JC = 120;
-// One record per stage, N + 1 per problem: record k = [Linv_k packed (171) | C_{k-1} (216; record
-// 0's unused) | compact J_k (120; record N-1's and N's unused)].  The forward sweep's step k reads
-// record k as it is; the backward sweep's step k needs C_k, which is record k+1's C — the same
-// element offsets plus one record for the C part.  So a step's blocks are one base pointer and
-// per-lane constant offsets (no per-element pointer selects).
-constexpr int ADM_REC = ADM_LP + 216 + ADM_JC, REC_C = ADM_LP, REC_J = ADM_LP + 216;
+// One record per stage, N per problem (problem b's at R + b N ADM_REC): [Linv_k packed lower
+// (171) | compact J_k (120) | pad (1)] = 292 doubles, 16-byte aligned.  k_admm_iter streams it
+// twice per OSQP iteration (forward and backward sweep); the coupling C_k = M_{k+1,k} Linv_k' of
+// the factor is never stored: the sweeps apply it as re I_{k+1} J_k and the triangular pair.
+constexpr int ADM_REC = 292, REC_J = ADM_LP;
 __device__ __forceinline__ int adm_tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // dense 12 x 18 J_k into LDS from its compact form
 __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
@@ -97,53 +97,6 @@ __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l)
     if (i < 6) v = j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
     else v = Jc[12 + 18 * (i - 6) + j];
     sJ[e] = v;
-  }
-}
-// dense 18 x 18 lower-triangular Linv into LDS from its packed form
-__device__ __forceinline__ void adm_stage_L(double* sL, const double* Lp, int l) {
-  for (int e = l; e < 324; e += 64) {
-    const int i = e / 18, j = e - 18 * i;
-    sL[e] = j <= i ? Lp[adm_tri(i, j)] : 0.0;
-  }
-}
-// A sweep step's blocks as one index space of ADM_ST doubles: packed Linv (171) | C (216) |
-// compact J (120); element e of it goes to LDS position adm_pf_dst(e) of [Linv 18 x 18 | C 12 x 18 |
-// J 12 x 18] (-1: beyond the space)
-constexpr int ADM_ST = ADM_LP + 216 + ADM_JC;
-__device__ __forceinline__ int adm_pf_dst(int e) {
-  if (e < ADM_LP) {
-    int i = 0;
-    while ((i + 1) * (i + 2) / 2 <= e) ++i;
-    return 18 * i + (e - i * (i + 1) / 2);
-  }
-  if (e < ADM_LP + 216) return 324 + (e - ADM_LP);
-  if (e < ADM_ST) {
-    const int c = e - ADM_LP - 216;
-    if (c < 6) return 540 + 18 * c + c;
-    if (c < 12) return 540 + 18 * (c - 6) + c;
-    return 540 + 18 * (6 + (c - 12) / 18) + (c - 12) % 18;
-  }
-  return -1;
-}
-// A lane's element t of a step: its record offset for the forward sweep (bits 0-9), for the
-// backward sweep (bits 10-19) and its LDS slot + 1 (bits 20-29; 0 = none), packed in one register.
-__device__ __forceinline__ int adm_pf_code(int e) {
-  if (e >= ADM_ST) return 0;
-  const int ob = e + (e >= REC_C && e < REC_J ? ADM_REC : 0);
-  return e | (ob << 10) | ((adm_pf_dst(e) + 1) << 20);
-}
-// one unconditional load per element from a record base and the lane's fixed offsets (lanes past
-// the space re-read the base): no branches around the loads, so the wait for them is a counted
-// vmcnt, not a vmcnt(0) at a control-flow join.  sh: 0 forward offsets, 10 backward.
-__device__ __forceinline__ void adm_pf_load(double pf[8], const double* rec, const int code[8], int sh) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) pf[t] = rec[(code[t] >> sh) & 1023];
-}
-__device__ __forceinline__ void adm_pf_store(const double pf[8], double* sB, const int code[8]) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int d = code[t] >> 20;
-    if (d) sB[d - 1] = pf[t];
   }
 }
 
@@ -198,16 +151,21 @@ __device__ __forceinline__ double adm_jc(const double* Jc, int i, int j) {
   return Jc[12 + 18 * (i - 6) + j];
 }
 
-__device__ __forceinline__ double adm_wave_max(double v) {
+// max / sum over groups of W lanes (W = 64: the wave; 16: a DPP row)
+template <int W>
+__device__ __forceinline__ double adm_max(double v) {
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  for (int off = W / 2; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, W));
   return v;
 }
-__device__ __forceinline__ double adm_wave_sum(double v) {
+template <int W>
+__device__ __forceinline__ double adm_sum(double v) {
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  for (int off = W / 2; off >= 1; off >>= 1) v += __shfl_xor(v, off, W);
   return v;
 }
+__device__ __forceinline__ double adm_wave_max(double v) { return adm_max<64>(v); }
+__device__ __forceinline__ double adm_wave_sum(double v) { return adm_sum<64>(v); }
 __device__ __forceinline__ double adm_limit(double v) { return v < 1e-4 ? 1.0 : (v > 1e4 ? 1e4 : v); }
 
 // unscaled J_k = [[I, dt I, 0], [Aq, Av, Bu]] (rows of A's block k+1 on z_k; src/osqp_solver.py:
@@ -236,7 +194,9 @@ __device__ __forceinline__ void adm_sweep_sync() {
 }
 
 // OSQP's check_termination on the unscaled residuals (+ the duality gap) and, for adapt_rho,
-// the scaled residual ratios; x, z, y scaled.  Returns solved; rho_est gets the estimate.
+// the scaled residual ratios; x, z, y scaled.  Returns solved; rho_est gets the estimate.  W lanes
+// share one problem (lane l of W): 64 (one problem per wave) or 16 (k_admm_iter: a 16-lane row).
+template <int W>
 __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, double rho, const double* x,
                           const double* z, const double* y, const double* qs, const double* ls, const double* D,
                           const double* E, const double* Jb, const double* Ib, const double* Pq, const double* Pd,
@@ -244,7 +204,7 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
   double pr = 0.0, zn = 0.0, an = 0.0, pri = 0.0, pn = 0.0;
   double dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0, dua = 0.0, dn = 0.0, xPx = 0.0, qx = 0.0, sc = 0.0;
   // rows: block 0 = I x_0, block k+1 = J_k z_k + I x_{k+1}
-  for (int r = l; r < m; r += 64) {
+  for (int r = l; r < m; r += W) {
     const int k = r / 12, i = r - 12 * k;
     double ax;
     if (k == 0) {
@@ -264,7 +224,7 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     pn = fmax(pn, fmax(fabs(z[r]), fabs(ax)));
     sc += ls[r] * fmax(y[r], 0.0) + ls[r] * fmin(y[r], 0.0);
   }
-  for (int e = l; e < T; e += 64) {
+  for (int e = l; e < T; e += W) {
     const int k = e / 18, j = e - 18 * k;
     double px;
     if (j < 6) {
@@ -289,10 +249,10 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     xPx += x[e] * px;
     qx += qs[e] * x[e];
   }
-  pr = adm_wave_max(pr); zn = adm_wave_max(zn); an = adm_wave_max(an); pri = adm_wave_max(pri); pn = adm_wave_max(pn);
-  dr = adm_wave_max(dr); qn = adm_wave_max(qn); atn = adm_wave_max(atn); pxn = adm_wave_max(pxn);
-  dua = adm_wave_max(dua); dn = adm_wave_max(dn);
-  xPx = adm_wave_sum(xPx); qx = adm_wave_sum(qx); sc = adm_wave_sum(sc);
+  pr = adm_max<W>(pr); zn = adm_max<W>(zn); an = adm_max<W>(an); pri = adm_max<W>(pri); pn = adm_max<W>(pn);
+  dr = adm_max<W>(dr); qn = adm_max<W>(qn); atn = adm_max<W>(atn); pxn = adm_max<W>(pxn);
+  dua = adm_max<W>(dua); dn = adm_max<W>(dn);
+  xPx = adm_sum<W>(xPx); qx = adm_sum<W>(qx); sc = adm_sum<W>(sc);
   const double cinv = 1.0 / c;
   // OSQP compute_rho_estimate (scaled residuals)
   {
@@ -485,7 +445,7 @@ __device__ __forceinline__ double adm_readlane(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane((int)u, lane), hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
+__device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
                            double* Rb, double* sS, double* sJ, double* sL, double* sCp, int l0) {
   const double re = 1e3 * rho, sigma = a.A.sigma;
   const int T = 18 * N - 6;
@@ -572,7 +532,6 @@ __device__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* P
           const double acc = adm_dot2<18>(0.0, sJ + 18 * i, 1, sL + 18 * j, 1);
           const double cv = re * Ib[12 * (k + 1) + i] * acc;
           sCp[FS * i + j] = cv;
-          Rb[ADM_REC * (k + 1) + REC_C + e] = cv;
         }
       }
     }
@@ -650,58 +609,42 @@ __device__ void adm_factor_lds(const AdmmArgs& a, int N, double rho, const doubl
         for (int q = 0; q <= j; ++q) acc += sJ[18 * i + q] * sL[18 * j + q];
         const double cv = re * Ib[12 * (k + 1) + i] * acc;
         sCp[e] = cv;
-        Rb[ADM_REC * (k + 1) + REC_C + e] = cv;
       }
     }
     wave_sync_all();
   }
 }
 
-// The QP in three launches: k_admm_scale (PH 1: scaling, the new q and l; c to a.cs), k_admm_factor
-// (PH 8: the block Cholesky) and k_admm_iter (PH 2: OSQP's iterations and the output; PH 4: with
-// adaptive rho, whose re-factor needs the factor's registers and LDS — without it the iteration
-// kernel is compiled lean).  Each is compiled for its own registers and LDS.
+// k_admm_scale (PH 1: scaling, the new q and l; c to a.cs) and k_admm_factor (PH 8: the block
+// Cholesky), one problem per wave; each compiled for its own registers and LDS.
 template <int PH, int CT>
 __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   const int b = a.b0 + blockIdx.x;
   const SolveParams& P = a.P;
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
-  constexpr bool FAC = (PH & 8) || (PH & 4);
-  // (k_admm_prep: sB holds the column scale factors of a Ruiz pass before the factor needs it)
-  __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1], sR[32], sW[32], sT0[16], sT1[16];
+  constexpr bool FAC = (PH & 8) != 0;
+  // (k_admm_scale: sB holds the column scale factors of a Ruiz pass)
+  __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1];
   __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1];
   double* sL = sB;
-  double* sC = sB + 324;
   double* sJ = sB + 540;
   const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
   const double* CO = a.cost + (long)b * N * COST_STRIDE;
   const double* QD = a.qpd + (long)b * (N - 1) * QPD_STRIDE;
   const double* X = a.xu + (long)b * T;
-  double* x = a.sx + (long)b * T;
-  double* z = a.sz + (long)b * m;
-  double* y = a.sy + (long)b * m;
   double* qold = a.sq + (long)b * T;
   double* Pq = a.Pq + (long)b * N * 36;
   double* Pd = a.Pd + (long)b * T;
-#ifdef I7M_DIAG_ADMM_SHARED_REC  // (timing builds only: every problem's iterations read problem 0's stage records)
-  double* Rb = a.R + (long)((PH & 2) ? 0 : b) * (N + 1) * ADM_REC;
-#else
-  double* Rb = a.R + (long)b * (N + 1) * ADM_REC;
-#endif
+  double* Rb = a.R + (long)b * N * ADM_REC;
   double* Jb = Rb + REC_J;  // J_k at Jb + ADM_REC k
   double* Ib = a.I + (long)b * m;
   double* qs = a.qs + (long)b * T;
   double* ls = a.ls + (long)b * m;
   double* D = a.D + (long)b * T;
   double* E = a.E + (long)b * m;
-
-  double* wv = a.w + (long)b * T;
-  const double dt = P.dt;
-
-  double c = 1.0;
   if constexpr (PH & 1) {
-    c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
+    const double c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
     if (l == 0) a.cs[b] = c;
   }
   if constexpr (PH & 8) {
@@ -711,169 +654,503 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
     adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
 #endif
   }
-  if constexpr (PH & 2) {
-  if constexpr (!(PH & 1)) {
-    // the LDS slots no sweep step writes (Linv's upper triangle, J's q-row zeros) are zeros
-    for (int e = l; e < 324 + 216 + 216; e += 64) sB[e] = 0.0;
-  }
-  c = a.cs[b];
-  double rho = a.srho[b];
-  double rv = 1e3 * rho, ri = 1.0 / rv;
-  const double al = a.A.alpha, sg = a.A.sigma;
+}
 
-  // ---- 3. OSQP iterations
-  // Each sweep step stages the stage's blocks (packed Linv_k | C | compact J_k: ADM_ST doubles)
-  // through LDS.  Everything the next step reads from HBM — its blocks (8 doubles per lane) and
-  // its vector entries (x, q, the -I entries, z, y, l of the rows it finishes) — is loaded into
-  // registers at the start of this step, before this step's stores, so the loads' latency hides
-  // behind the step and waiting for them never waits for a store (vmcnt is in order).  The LDS
-  // slots' fixed zeros (Linv's upper triangle, J's q-row zeros) are set above.
-  int pcode[8];
+// ---- OSQP's iterations (k_admm_iter): four problems per wave, one per 16-lane DPP row --------
+// Lane l works on problem b0 + 4 blockIdx.x + (l >> 4), row c = l & 15 of its 18-dim stage vectors:
+// a stage vector v is (v_lo in lane c = v_c, c < 16; v16, v17 held by every lane of the row).  The
+// sweeps are the block LDL' of M with S_k^-1 = Linv_k' Linv_k (oracle/cpp/i7m_cpu.cpp admm_solve):
+//   forward   g_k = rhs_k - [re I_k (J_{k-1} h_{k-1}); 0],  h_k = Linv_k' (Linv_k g_k)
+//   backward  xt_k = h_k - Linv_k' (Linv_k (J_k' (re I_{k+1} xt_{k+1}[:12])))
+// then z~ = J_k xt_k + I_{k+1} xt_{k+1} for block k+1's rows, OSQP's relaxation, projection and dual
+// update.  Every mat-vec is a chain of fma's whose broadcast operand comes from the row's own lanes
+// by DPP (v_mov_b64_dpp row_newbcast: no LDS round trip on the sweep's chain); the matrix operand
+// is read from the stage's LDS image.  Each step's stage record (Linv packed | compact J: 292
+// doubles per problem, 10 dwordx4 per lane) is loaded two steps ahead into registers, then
+// scattered into a dense LDS image (Linv 18 x 18, J 12 x 18, zeros fixed) at the step's start; the
+// step's vectors ride in the same ring.  Problems stop at their own termination test; a finished
+// row keeps shadowing the others' loads (its addresses are a running row's) and stores nothing.
+constexpr int A4_PS = 541;  // doubles of one problem's LDS image (Linv 324 | J 216 | zero); odd:
+                            // two problems of a lane half read disjoint banks
+constexpr int A4_LJ = 324;
+template <int n>
+__device__ __forceinline__ double a4_bc(double v) {  // lane n of the 16-lane row, to every lane of it
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + n, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double a4_dpp32(double v, int ctrl_is_shl) {
+  const long long u = __double_as_longlong(v);
+  int lo = (int)u, hi = (int)(u >> 32);
+  if (ctrl_is_shl) {
+    lo = __builtin_amdgcn_update_dpp(lo, lo, 0x106, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, 0x106, 0xf, 0xf, false);
+  } else {
+    lo = __builtin_amdgcn_update_dpp(lo, lo, 0x116, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, 0x116, 0xf, 0xf, false);
+  }
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// lane c gets lane c - 6's value (c >= 6 of the row), keeps its own below / lane c + 6's (c < 10)
+__device__ __forceinline__ double a4_shr6(double v) { return a4_dpp32(v, 0); }
+__device__ __forceinline__ double a4_shl6(double v) { return a4_dpp32(v, 1); }
+template <int I, int N, class F>
+__device__ __forceinline__ void a4_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    a4_for<I + 1, N>(f);
+  }
+}
+struct A4Vec {
+  double lo, h16, h17;
+};
+// acc += (lane n of the row's v) * coef: v_fmac_f64_dpp with the broadcast fused (DP DPP takes only
+// row_newbcast).  Four fma's per statement into four accumulators; the statement opens with the
+// two wait states a DPP read of a VGPR a VALU just wrote needs (the compiler pads no asm).
+template <int n>
+__device__ __forceinline__ void a4_fmac4(double& a0, double& a1, double& a2, double& a3, double v, double c0, double c1,
+                                         double c2, double c3) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:%9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %4, %6 row_newbcast:%10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %2, %4, %7 row_newbcast:%11 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %3, %4, %8 row_newbcast:%12 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+      : "v"(v), "v"(c0), "v"(c1), "v"(c2), "v"(c3), "i"(n), "i"(n + 1), "i"(n + 2), "i"(n + 3));
+}
+template <int n>
+__device__ __forceinline__ void a4_fmac2(double& a0, double& a1, double v, double c0, double c1) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1)
+      : "v"(v), "v"(c0), "v"(c1), "i"(n), "i"(n + 1));
+}
+// sum_{l < 16} coef[l] * v_l as four interleaved chains (l mod 4), combined (a0 + a1) + (a2 + a3):
+// the device's and the port's order (oracle/cpp/i7m_cpu.cpp dot16)
+__device__ __forceinline__ double a4_dot16(double v, const double* cf) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  a4_fmac4<0>(a0, a1, a2, a3, v, cf[0], cf[1], cf[2], cf[3]);
+  a4_fmac4<4>(a0, a1, a2, a3, v, cf[4], cf[5], cf[6], cf[7]);
+  a4_fmac4<8>(a0, a1, a2, a3, v, cf[8], cf[9], cf[10], cf[11]);
+  a4_fmac4<12>(a0, a1, a2, a3, v, cf[12], cf[13], cf[14], cf[15]);
+  return __dadd_rn(__dadd_rn(a0, a1), __dadd_rn(a2, a3));
+}
+// sum_{r = 6..11} coef[r - 6] * u_r as two chains (r even / odd), combined
+__device__ __forceinline__ double a4_dot6(double u, const double* cf) {
+  double a0 = 0.0, a1 = 0.0;
+  a4_fmac2<6>(a0, a1, u, cf[0], cf[1]);
+  a4_fmac2<8>(a0, a1, u, cf[2], cf[3]);
+  a4_fmac2<10>(a0, a1, u, cf[4], cf[5]);
+  return __dadd_rn(a0, a1);
+}
+// One stage image's coefficients of a lane, read from LDS at the step's start (all reads issued
+// before the first fma: one LDS latency per step, not one per chain)
+struct A4Coef {
+  double L[16], L16[17], L17[18];   // Linv row c, rows 16 and 17 (lmul)
+  double Lt[16], Lt16c, Lt17c;      // Linv column c (l < 16), L[16][c], L[17][c] (ltmul)
+  double l1616, l1716, l1717;       // the (16, 17) block (ltmul)
+  double Jt[6], J16[6], J17[6], Jd; // J column c (rows 6..11), columns 16, 17 (rows 6..11), J[c % 6][c] (jtmul)
+  double Jr[18], Jq0, Jq1;          // J row c (c in 6..11; row 11 above), J[q][q], J[q][6 + q] (jmul, q = c < 6 ? c : 0)
+};
+__device__ __forceinline__ void a4_coef(A4Coef& C, const double* Lb, int c) {
+  const double* Jb = Lb + A4_LJ;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) pcode[t] = adm_pf_code(l + 64 * t);
-  int it;
+  for (int l = 0; l < 16; ++l) C.L[l] = Lb[18 * c + l];
+#pragma unroll
+  for (int l = 0; l < 17; ++l) C.L16[l] = Lb[18 * 16 + l];
+#pragma unroll
+  for (int l = 0; l < 18; ++l) C.L17[l] = Lb[18 * 17 + l];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) C.Lt[l] = Lb[18 * l + c];
+  C.Lt16c = Lb[18 * 16 + c];
+  C.Lt17c = Lb[18 * 17 + c];
+  C.l1616 = Lb[18 * 16 + 16];
+  C.l1716 = Lb[18 * 17 + 16];
+  C.l1717 = Lb[18 * 17 + 17];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    C.Jt[r] = Jb[18 * (6 + r) + c];
+    C.J16[r] = Jb[18 * (6 + r) + 16];
+    C.J17[r] = Jb[18 * (6 + r) + 17];
+  }
+  C.Jd = Jb[18 * (c % 6) + c];
+  const int rr = c < 12 ? c : 11;
+#pragma unroll
+  for (int l = 0; l < 18; ++l) C.Jr[l] = Jb[18 * rr + l];
+  const int q = c < 6 ? c : 0;
+  C.Jq0 = Jb[18 * q + q];
+  C.Jq1 = Jb[18 * q + 6 + q];
+}
+// y = Linv v
+__device__ __forceinline__ A4Vec a4_lmul(const A4Coef& C, const A4Vec& v) {
+  const double lo = a4_dot16(v.lo, C.L);
+  double b16 = a4_dot16(v.lo, C.L16), b17 = a4_dot16(v.lo, C.L17);
+  b16 = __fma_rn(C.L16[16], v.h16, b16);
+  b17 = __fma_rn(C.L17[16], v.h16, b17);
+  b17 = __fma_rn(C.L17[17], v.h17, b17);
+  return {lo, b16, b17};
+}
+// y = Linv' v
+__device__ __forceinline__ A4Vec a4_ltmul(const A4Coef& C, const A4Vec& v) {
+  double lo = a4_dot16(v.lo, C.Lt);
+  lo = __fma_rn(C.Lt16c, v.h16, lo);
+  lo = __fma_rn(C.Lt17c, v.h17, lo);
+  return {lo, __fma_rn(C.l1716, v.h17, __dmul_rn(C.l1616, v.h16)), __dmul_rn(C.l1717, v.h17)};
+}
+// init + J' u: the q-row entry of column c (J[c % 6][c], zero for c >= 12) with u[c % 6], plus the
+// v rows 6..11 (two chains); u in lanes 0..11, every lane's finite
+__device__ __forceinline__ A4Vec a4_jtmul(const A4Coef& C, double u, A4Vec init) {
+  const double us = a4_shr6(u);  // u[c - 6] for c >= 6, own below
+  const double lo = __dadd_rn(__fma_rn(C.Jd, us, init.lo), a4_dot6(u, C.Jt));
+  return {lo, __dadd_rn(init.h16, a4_dot6(u, C.J16)), __dadd_rn(init.h17, a4_dot6(u, C.J17))};
+}
+// (J v)_c, c < 12 (lanes 12-15: row 11's, unused)
+__device__ __forceinline__ double a4_jmul(const A4Coef& C, int c, const A4Vec& v) {
+  double a = a4_dot16(v.lo, C.Jr);
+  a = __fma_rn(C.Jr[16], v.h16, a);
+  a = __fma_rn(C.Jr[17], v.h17, a);
+  const double sp = __fma_rn(C.Jq1, a4_shl6(v.lo), __dmul_rn(C.Jq0, v.lo));
+  return c < 6 ? sp : a;
+}
+
+// The ring buffer of one step: the stage record (this lane's 10 chunks) and the step's vectors.
+struct A4Buf {
+  double2 rec[10];  // chunks c + 16 t of the lane's problem's stage record
+  double v0, v1, z1, y1, l1, ib1;
+  double2 hv0, hv1;
+};
+
+// Buffer-resource access (uniform base in SGPRs, 32-bit per-lane offset, hardware range check): a
+// store or load at an offset past the range does nothing (loads return 0), which masks the stores
+// of finished rows and of absent rows without branches.
+typedef unsigned int a4u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int a4u4 __attribute__((ext_vector_type(4)));
+constexpr int A4_OOB = 1 << 27;  // doubles: beyond every range
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t a4_rsrc(const void* base, long bytes) {
+  const unsigned long long u = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
+__device__ __forceinline__ double a4_ld(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off * 8, 0, 0));
+}
+__device__ __forceinline__ double2 a4_ld2(__amdgpu_buffer_rsrc_t r, int off) {
+  const a4u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off * 8, 0, 0);
+  return make_double2(__builtin_bit_cast(double, a4u2{v.x, v.y}), __builtin_bit_cast(double, a4u2{v.z, v.w}));
+}
+__device__ __forceinline__ void a4_st(double v, __amdgpu_buffer_rsrc_t r, int off) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(a4u2, v), r, off * 8, 0, 0);
+}
+
+// OSQP's iteration loop of one wave (four problems).  Per-lane state lives in registers; the
+// arrays are per-wave buffer resources (SGPRs) with small per-lane offsets.
+template <bool ADAPT>
+__device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
+  const SolveParams& P = a.P;
+  const int N = P.N, T = P.T, m = 12 * N;
+  const int l = threadIdx.x, p = l >> 4, c = l & 15;
+  __shared__ double sImg[4 * A4_PS];
+  double* Lb = sImg + A4_PS * p;  // this problem's stage image: Linv dense (18 x 18), J dense at +324
+  const int bb = a.b0 + 4 * (int)blockIdx.x;
+  bool run = bb + p < P.B && !(a.active && !a.active[bb + p]);
+  const bool act = run;
+  if (!__ballot(run)) return;
+  // the wave's four problems' rows of every array
+  const long wT = (long)bb * T, wm = (long)bb * m, wR = (long)bb * N * ADM_REC;
+  const auto rX = a4_rsrc(a.sx + wT, 32L * T), rZ = a4_rsrc(a.sz + wm, 32L * m), rY = a4_rsrc(a.sy + wm, 32L * m);
+  const auto rQ = a4_rsrc(a.qs + wT, 32L * T), rL = a4_rsrc(a.ls + wm, 32L * m), rI = a4_rsrc(a.I + wm, 32L * m);
+  const auto rH = a4_rsrc(a.w + wT, 32L * T), rR = a4_rsrc(a.R + wR, 32L * N * ADM_REC);
+  int prow = p;  // the row whose problem this lane's loads read (a finished or idle row reads a running one's)
+  auto pick_shadow = [&]() {
+    const unsigned long long any = __ballot(run);
+    if (any && !run) prow = (__ffsll((long long)any) - 1) >> 4;
+  };
+  pick_shadow();
+  int oT = prow * T, om = prow * m, oR = prow * N * ADM_REC;
+  const int bown = bb + p;
+  const double c_cost = a.cs[bb + prow];
+  double rho = a.srho[bb + prow];
+  double rv = 1e3 * rho, ri = 1.0 / rv;
+  const double al = a.A.alpha, sg = a.A.sigma, al1 = 1.0 - al;
+  for (int e = l; e < 4 * A4_PS; e += 64) sImg[e] = 0.0;
+  // this lane's chunk destinations in the image (packed Linv -> 18 i + j, compact J -> 324 + 18 i + j)
+  int dst[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+    int code = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int e = 2 * (c + 16 * t) + h;
+      if (e > ADM_REC - 1) e = ADM_REC - 1;
+      int d;
+      if (e < ADM_LP) {
+        int i = 0;
+        while ((i + 1) * (i + 2) / 2 <= e) ++i;
+        d = 18 * i + (e - i * (i + 1) / 2);
+      } else if (e < ADM_LP + ADM_JC) {
+        const int q = e - ADM_LP;
+        if (q < 6) d = A4_LJ + 19 * q;
+        else if (q < 12) d = A4_LJ + 18 * (q - 6) + q;
+        else d = A4_LJ + 18 * (6 + (q - 12) / 18) + (q - 12) % 18;
+      } else {
+        d = A4_PS - 1;
+      }
+      code |= d << (16 * h);
+    }
+    dst[t] = code;
+  }
+  const int cc = c < 12 ? c : 11;
+  const int c16 = 16 + (c & 1);  // lanes 0, 1 store the u-part pair (16, 17)
+  const bool lo12 = c < 12, lo2 = c < 2;
+  int chk_off[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) chk_off[t] = 2 * ((c + 16 * t) < 146 ? c + 16 * t : 145);
+  // the loads of step s (< 2N) of an iteration: its stage record; forward: x_k, q_k; backward: h_k,
+  // x_{k+1}; both: block k+1's z, y, l, I.  Every index in bounds (the last stage's missing rows
+  // and u-parts read a neighbour, unused).
+  auto issue = [&](A4Buf& B, int s) {
+    const bool fwd = s < N;
+    const int k = fwd ? s : 2 * N - 1 - s;
+    const int k1 = k + 1 < N ? k + 1 : N - 1;
+    const int kh = k < N - 1 ? k : N - 2;
+#ifdef I7M_DIAG
+    // I7M_ABLATE 21: every step reads stage 0's record (L2-resident: the sweep without its stream)
+    const int ro = oR + (a.ablate == 21 ? 0 : k * ADM_REC);
+#else
+    const int ro = oR + k * ADM_REC;
+#endif
+#pragma unroll
+    for (int t = 0; t < 10; ++t) B.rec[t] = a4_ld2(rR, ro + chk_off[t]);
+    const int ci = k < N - 1 ? c : cc;
+    const int kb = fwd ? k : k1;  // the stage of v1
+    const int kbh = kb < N - 1 ? kb : N - 2;
+    const int cb = kb < N - 1 ? c : cc;
+    if (fwd) {
+      B.v0 = a4_ld(rX, oT + 18 * k + ci);
+      B.v1 = a4_ld(rQ, oT + 18 * kb + cb);
+      B.hv0 = a4_ld2(rX, oT + 18 * kh + 16);
+      B.hv1 = a4_ld2(rQ, oT + 18 * kbh + 16);
+    } else {
+      B.v0 = a4_ld(rH, oT + 18 * k + ci);
+      B.v1 = a4_ld(rX, oT + 18 * kb + cb);
+      B.hv0 = a4_ld2(rH, oT + 18 * kh + 16);
+      B.hv1 = a4_ld2(rX, oT + 18 * kbh + 16);
+    }
+    const int ob = om + 12 * k1 + cc;
+    B.z1 = a4_ld(rZ, ob);
+    B.y1 = a4_ld(rY, ob);
+    B.l1 = a4_ld(rL, ob);
+    B.ib1 = a4_ld(rI, ob);
+  };
+  auto scatter = [&](const A4Buf& B) {
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      Lb[dst[t] & 0xffff] = B.rec[t].x;
+      Lb[dst[t] >> 16] = B.rec[t].y;
+    }
+  };
+  A4Buf A0, A1;
+  issue(A0, 0);
+  issue(A1, 1);
+  // carried between steps
+  A4Vec hc{0.0, 0.0, 0.0};  // forward: J_{k-1} h_{k-1} (lanes 0..11) / backward: xt_{k+1}
+  double tk = __dmul_rn(rv, __dsub_rn(a4_ld(rZ, om + cc), __dmul_rn(ri, a4_ld(rY, om + cc))));  // block k's t
+  double ibk = a4_ld(rI, om + cc);
+  // the state the backward sweep hands to the next forward sweep's first two steps (their memory
+  // copies were loaded before the backward sweep wrote them)
+  double nx0 = 0.0, nx1 = 0.0, nz1 = 0.0, ny1 = 0.0;
+  double2 nx0h = make_double2(0.0, 0.0), nx1h = make_double2(0.0, 0.0);
+  int done_it = 0;
   bool solved = false;
-  const bool lx = l < 18, lr = l < 12;
+  // one step's start: the record into the image, the step's vectors out of the ring, the ring
+  // advanced and the load of step s + 2 issued
+  double v0, v1, z1, y1, l1, ib1;
+  double2 hv0, hv1;
+  A4Coef C;
+  auto begin = [&](int s) {
+    __asm__ volatile("" ::: "memory");
+    scatter(A0);
+    __asm__ volatile("" ::: "memory");
+    a4_coef(C, Lb, c);
+    v0 = A0.v0; v1 = A0.v1; z1 = A0.z1; y1 = A0.y1; l1 = A0.l1; ib1 = A0.ib1; hv0 = A0.hv0; hv1 = A0.hv1;
+    A0 = A1;
+    int sn = s + 2;
+    if (sn >= 2 * N) sn -= 2 * N;
+    issue(A1, sn);
+  };
+  // store offsets: masked (past the range) for rows that do not run
+  auto so = [&](bool ok, int off) { return run && ok ? off : A4_OOB; };
+  // forward step k < N - 1: rhs, g, h = Linv' Linv g (stored), the next coupling J_k h
+  auto fwd = [&](int k) {
+    const double t1 = __dmul_rn(rv, __dsub_rn(z1, __dmul_rn(ri, y1)));
+    const double init = lo12 ? __dmul_rn(ibk, tk) : 0.0;
+    A4Vec r = a4_jtmul(C, t1, A4Vec{init, 0.0, 0.0});
+    r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
+    r.h16 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.x), hv1.x), r.h16);
+    r.h17 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.y), hv1.y), r.h17);
+    const double rc = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));  // k = 0: hc = 0
+    r.lo = lo12 ? rc : r.lo;
+    const A4Vec h = a4_ltmul(C, a4_lmul(C, r));
+    a4_st(h.lo, rH, so(true, oT + 18 * k + c));
+    a4_st(c == 0 ? h.h16 : h.h17, rH, so(lo2, oT + 18 * k + c16));
+    hc.lo = a4_jmul(C, c, h);
+    tk = t1;
+    ibk = ib1;
+  };
+  // the last forward step (k = N - 1: 12 rows, no J, no u-part)
+  auto fwd_last = [&]() {
+    const int k = N - 1;
+    A4Vec r{lo12 ? __dmul_rn(ibk, tk) : 0.0, 0.0, 0.0};
+    r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
+    r.lo = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));
+    r.lo = lo12 ? r.lo : 0.0;
+    hc = a4_ltmul(C, a4_lmul(C, r));  // the backward sweep starts from xt_{N-1} = h_{N-1}
+    a4_st(hc.lo, rH, so(lo12, oT + 18 * k + c));
+  };
+  // backward step k < N - 1: xt_k, then block k+1's rows and x_{k+1}
+  auto bwd = [&](int k) {
+    const double u = __dmul_rn(__dmul_rn(rv, ib1), hc.lo);
+    const A4Vec s2 = a4_ltmul(C, a4_lmul(C, a4_jtmul(C, u, A4Vec{0.0, 0.0, 0.0})));
+    const A4Vec xt{__dsub_rn(v0, s2.lo), __dsub_rn(hv0.x, s2.h16), __dsub_rn(hv0.y, s2.h17)};
+    const double zt = __dadd_rn(a4_jmul(C, c, xt), __dmul_rn(ib1, hc.lo));
+    const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z1));
+    double zn = __dadd_rn(zr, __dmul_rn(ri, y1));
+    zn = fmin(fmax(zn, l1), l1);
+    const double yn = __dadd_rn(y1, __dmul_rn(rv, __dsub_rn(zr, zn)));
+    const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, v1));
+    const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, hv1.x));
+    const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, hv1.y));
+    const bool last1 = k + 1 == N - 1;  // x_{k+1} has no u-part
+    const int ob = om + 12 * (k + 1) + c;
+    a4_st(zn, rZ, so(lo12, ob));
+    a4_st(yn, rY, so(lo12, ob));
+    a4_st(xn, rX, so(!last1 || lo12, oT + 18 * (k + 1) + c));
+    a4_st(c == 0 ? xn16 : xn17, rX, so(!last1 && lo2, oT + 18 * (k + 1) + c16));
+    if (k == 0) {
+      nx1 = xn;
+      nx1h = make_double2(xn16, xn17);
+      nz1 = zn;
+      ny1 = yn;
+    }
+    hc = xt;
+  };
+  int it;
   for (it = 1; it <= a.A.max_iter; ++it) {
-    // forward sweep: w_k = Linv_k (rhs_k - C_{k-1} w_{k-1})
-    // (the next step's loads are unconditional, at clamped stage / lane indices: in bounds always,
-    // unused where a stage has no such block or entry)
-    const int l17 = l < 17 ? l : 17, l11 = l < 11 ? l : 11;
-    double pf[8], fx, fq, fi, fz, fy;
-    adm_pf_load(pf, Rb, pcode, 0);
-    fx = x[l17];
-    fq = qs[l17];
-    fi = Ib[l11];
-    fz = z[12 + l11];
-    fy = y[12 + l11];
-    if (lr) sT0[l] = rv * (z[l] - ri * y[l]);
-    for (int k = 0; k < N; ++k) {
-      const int nk = k < N - 1 ? 18 : 12;
-      adm_sweep_sync();
-      adm_pf_store(pf, sB, pcode);
-      const double xe = fx, qe = fq, ie = fi, t1 = rv * (fz - ri * fy);
-      {
-        const int kn = k + 1 < N ? k + 1 : N - 1, kz = k + 2 < N ? k + 2 : N - 1;
-        adm_pf_load(pf, Rb + ADM_REC * kn, pcode, 0);
-        const int ln = kn < N - 1 ? l17 : l11;
-        fx = x[18 * kn + ln];
-        fq = qs[18 * kn + ln];
-        fi = Ib[12 * kn + l11];
-        fz = z[12 * kz + l11];
-        fy = y[12 * kz + l11];
+    int s = 0;
+    for (int k = 0; k < N - 1; ++k, ++s) {
+      begin(s);
+      if (it > 1 && k == 0) {
+        v0 = nx0; hv0 = nx0h; z1 = nz1; y1 = ny1;
       }
-      if (k < N - 1 && lr) sT1[l] = t1;
-      adm_sweep_sync();
-      if (l < nk) {
-        const int j = l;
-        double acc = j < 12 ? ie * sT0[j] : 0.0;
-        if (k < N - 1) acc = adm_dot<12>(acc, sJ + j, 18, sT1);
-        double r = (sg * xe - qe) + acc;
-        if (k > 0 && j < 12) r -= adm_dot<18>(0.0, sC + 18 * j, 1, sW);
-        sR[j] = r;
+      if (it > 1 && k == 1) {
+        v0 = nx1; hv0 = nx1h;
       }
-      adm_sweep_sync();
-      double wk = 0.0;
-      if (l < nk) {
-        wk = adm_dot<18>(0.0, sL + 18 * l, 1, sR);
-        wv[18 * k + l] = wk;
-      }
-      adm_sweep_sync();
-      if (l < nk) sW[l] = wk;
-      if (lr) sT0[l] = sT1[l];
+      fwd(k);
     }
-    // backward sweep: xt_k = Linv_k' (w_k - C_k' xt_{k+1}); then A xt for the rows of block k+1,
-    // the relaxation of x_{k+1}, and the projection and dual update of block k+1 (block 0 after
-    // the sweep).  xt never leaves registers: step k needs only xt_k and xt_{k+1}.  Every global
-    // value a lane reads it wrote itself (lane = index within the knot / block).
-    double bw, bz = 0.0, by = 0.0, bl = 0.0, bi = 0.0, bx = 0.0, xtp = 0.0;
-    adm_pf_load(pf, Rb + ADM_REC * (N - 1), pcode, 10);
-    bw = wv[18 * (N - 1) + l11];
-    for (int k = N - 1; k >= 0; --k) {
-      const int nk = k < N - 1 ? 18 : 12;
-      adm_sweep_sync();
-      adm_pf_store(pf, sB, pcode);
-      const double we = bw, zr0 = bz, yr0 = by, lr0 = bl, ir0 = bi, xe1 = bx;
-      // step k - 1's loads: its blocks, w_{k-1}, block k's rows, x_k (block 0's rows and x_0 at
-      // k = 0: there the block loads re-read stage 0, unused)
-      {
-        const int kp = k > 0 ? k - 1 : 0;
-        adm_pf_load(pf, Rb + ADM_REC * kp, pcode, 10);
-        bw = wv[18 * kp + l17];
-        bz = z[12 * k + l11];
-        by = y[12 * k + l11];
-        bl = ls[12 * k + l11];
-        bi = Ib[12 * k + l11];
-        bx = x[18 * k + (k < N - 1 ? l17 : l11)];
-      }
-      adm_sweep_sync();
-      if (l < nk) {
-        double r = we;
-        if (k < N - 1) r -= adm_dot<12>(0.0, sC + l, 18, sW);
-        sR[l] = r;
-      }
-      adm_sweep_sync();
-      double xk = 0.0;
-      if (l < nk) xk = adm_dot<18>(0.0, sL + l, 18, sR);
-      // sW holds xt_{k+1}'s x part until block k+1's rows are done; sR takes xt_k once every lane
-      // has read the right-hand side
-      adm_sweep_sync();
-      if (l < nk) sR[l] = xk;
-      adm_sweep_sync();
-      if (k < N - 1 && lr) {
-        const int r = 12 * (k + 1) + l;
-        const double zt = adm_dot<18>(0.0, sJ + 18 * l, 1, sR) + ir0 * sW[l];
-        const double zr = al * zt + (1.0 - al) * zr0;
-        double zn = zr + ri * yr0;
-        zn = fmin(fmax(zn, lr0), lr0);
-        y[r] = yr0 + rv * (zr - zn);
-        z[r] = zn;
-      }
-      if (k < N - 1) {
-        const int nn = k + 1 < N - 1 ? 18 : 12;
-        if (l < nn) x[18 * (k + 1) + l] = al * xtp + (1.0 - al) * xe1;
-      }
-      xtp = xk;
-      adm_sweep_sync();
-      if (lr) sW[l] = sR[l];
+    begin(s++);
+    if (it > 1 && N == 2) v0 = nx1;  // (N = 2: the last forward step is stage 1)
+    fwd_last();
+    begin(s++);  // backward k = N - 1: xt_{N-1} = h_{N-1} (in hc), nothing else
+    for (int k = N - 2; k >= 0; --k, ++s) {
+      begin(s);
+      bwd(k);
     }
-    // block 0 rows and x_0 (their old values were loaded at k = 0)
-    if (lr) {
-      const double zt = bi * sW[l];
-      const double zr = al * zt + (1.0 - al) * bz;
-      double zn = zr + ri * by;
-      zn = fmin(fmax(zn, bl), bl);
-      y[l] = by + rv * (zr - zn);
-      z[l] = zn;
+    // block 0's rows (z~ = I xt_0) and x_0
+    {
+      const double z0 = a4_ld(rZ, om + cc), y0 = a4_ld(rY, om + cc), l0 = a4_ld(rL, om + cc), i0 = a4_ld(rI, om + cc);
+      const double x0 = a4_ld(rX, oT + c);
+      const double2 x0h = a4_ld2(rX, oT + 16);
+      const double zt = __dmul_rn(i0, hc.lo);
+      const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z0));
+      double zn = __dadd_rn(zr, __dmul_rn(ri, y0));
+      zn = fmin(fmax(zn, l0), l0);
+      const double yn = __dadd_rn(y0, __dmul_rn(rv, __dsub_rn(zr, zn)));
+      const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, x0));
+      const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, x0h.x));
+      const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, x0h.y));
+      a4_st(zn, rZ, so(lo12, om + c));
+      a4_st(yn, rY, so(lo12, om + c));
+      a4_st(xn, rX, so(true, oT + c));
+      a4_st(c == 0 ? xn16 : xn17, rX, so(lo2, oT + c16));
+      nx0 = xn;
+      nx0h = make_double2(xn16, xn17);
+      tk = __dmul_rn(rv, __dsub_rn(zn, __dmul_rn(ri, yn)));
+      ibk = i0;
+      hc = A4Vec{0.0, 0.0, 0.0};
     }
-    if (lx) x[l] = al * xtp + (1.0 - al) * bx;
-    wave_sync_all();
     const bool chk = a.A.check && it % a.A.check == 0;
-    const bool adapt = a.A.adapt_interval && it % a.A.adapt_interval == 0;
+    const bool adapt = ADAPT && a.A.adapt_interval && it % a.A.adapt_interval == 0;
     if (chk || adapt) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       double rest = rho;
-      const bool ok = adm_check(a, N, T, m, c, rho, x, z, y, qs, ls, D, E, Jb, Ib, Pq, Pd, &rest, l);
-      if (chk && ok) {
+      const long bq = bb + prow;
+      const bool ok = adm_check<16>(a, N, T, m, c_cost, rho, a.sx + bq * T, a.sz + bq * m, a.sy + bq * m, a.qs + bq * T,
+                                    a.ls + bq * m, a.D + bq * T, a.E + bq * m, a.R + bq * N * ADM_REC + REC_J,
+                                    a.I + bq * m, a.Pq + bq * N * 36, a.Pd + bq * T, &rest, c);
+      bool fin = false;
+      if (chk && ok && run) {
+        run = false;
         solved = true;
-        break;
+        done_it = it;
+        fin = true;
       }
-      if constexpr (PH & 4) {
-        if (adapt && (rest > rho * a.A.adapt_tol || rest < rho / a.A.adapt_tol)) {
-          rho = rest;
-          rv = 1e3 * rho;
-          ri = 1.0 / rv;
-          adm_factor(a, N, rho, Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+      bool reload = false;
+      if constexpr (ADAPT) {
+        const bool moved = run && adapt && (rest > rho * a.A.adapt_tol || rest < rho / a.A.adapt_tol);
+        const unsigned long long mv = __ballot(moved);
+        if (mv) {
+          if (moved) {
+            rho = rest;
+            rv = 1e3 * rho;
+            ri = 1.0 / rv;
+          }
+          // re-factor the rows whose rho moved, one problem at a time on the whole wave (the
+          // image is the factor's scratch)
+          for (int q = 0; q < 4; ++q) {
+            if (!((mv >> (16 * q)) & 0xffff)) continue;
+            const long bq2 = bb + q;
+            const double rq = __shfl(rho, 16 * q, 64);
+            double* scr = sImg;
+            adm_factor(a, N, rq, a.Pq + bq2 * N * 36, a.Pd + bq2 * T, a.I + bq2 * m, a.R + bq2 * N * ADM_REC, scr,
+                       scr + 30 * I7M_ADMM_FSTRIDE + 388, scr + 30 * I7M_ADMM_FSTRIDE, scr + 18 * I7M_ADMM_FSTRIDE, l);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          for (int e = l; e < 4 * A4_PS; e += 64) sImg[e] = 0.0;
+          tk = __dmul_rn(rv, __dsub_rn(a4_ld(rZ, om + cc), __dmul_rn(ri, a4_ld(rY, om + cc))));
+          reload = true;
         }
       }
+      if (!__ballot(run)) break;
+      if (__ballot(fin)) {
+        // finished rows read a running row's lines from here on
+        pick_shadow();
+        oT = prow * T;
+        om = prow * m;
+        oR = prow * N * ADM_REC;
+        reload = true;
+      }
+      if (reload) {
+        issue(A0, 0);
+        issue(A1, 1);
+      }
     }
   }
-  if (l == 0) {
-    a.srho[b] = rho;
-    if (a.iters) a.iters[(long)b * 8 + a.sqp_iter] = it > a.A.max_iter ? a.A.max_iter : it;
-    if (a.status) a.status[(long)b * 8 + a.sqp_iter] = solved ? 1 : 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (c == 0 && act) {
+    a.srho[bown] = rho;
+    if (a.iters) a.iters[(long)bown * 8 + a.sqp_iter] = solved ? done_it : a.A.max_iter;
+    if (a.status) a.status[(long)bown * 8 + a.sqp_iter] = solved ? 1 : 0;
   }
-  double* so = a.sol + (long)b * T;
-  for (int e = l; e < T; e += 64) so[e] = D[e] * x[e];
+  if (act) {
+    const double* D = a.D + (long)bown * T;
+    const double* xo = a.sx + (long)bown * T;
+    double* so_ = a.sol + (long)bown * T;
+    for (int e = c; e < T; e += 16) so_[e] = D[e] * xo[e];
   }
 }
 
@@ -886,11 +1163,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
 }
+// four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ADAPT ? I7M_ADMM_WPE : I7M_ADMM_ITER_WPE,
-                                                                       ADAPT ? I7M_ADMM_WPE : I7M_ADMM_ITER_WPE)))
-k_admm_iter(AdmmArgs a) {
-  admm_body<ADAPT ? 6 : 2, 1>(a);
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {
+  admm_iter4<ADAPT>(a);
 }
 
 }  // namespace i7m

@@ -266,7 +266,7 @@ void admm_sizes(long N, long sz[ADM_NBUF]) {
   const long T = 18 * N - 6, m = 12 * N;
   const long v[ADM_NBUF] = {T, m, m, T, 1,                        // x z y q rho (state)
                             36 * N, T, m, T, m, T, m,               // Pq Pd I qs ls D E
-                            ADM_REC * (N + 1), T, 1};               // stage records, w, c
+                            ADM_REC * N, T, 1};                     // stage records, w (h), c
   for (int i = 0; i < ADM_NBUF; ++i) sz[i] = v[i];
 }
 // AdmmArgs pointers of problems [b0, ...) in the handle's ADMM allocation (array-of-buffers, each
@@ -278,7 +278,7 @@ AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
   double* cur = base;
   for (int i = 0; i < ADM_NBUF; ++i) {
     p[i] = cur + b0 * sz[i];
-    cur += Bm * sz[i];
+    cur += (Bm * sz[i] + 1) & ~1L;  // every buffer 16-byte aligned (k_admm_iter's 16-byte loads)
   }
   AdmmArgs a{};
   a.sx = p[0]; a.sz = p[1]; a.sy = p[2]; a.sq = p[3]; a.srho = p[4];
@@ -292,7 +292,7 @@ size_t admm_doubles(long Bm, long N) {
   long sz[ADM_NBUF];
   admm_sizes(N, sz);
   size_t t = 0;
-  for (int i = 0; i < ADM_NBUF; ++i) t += (size_t)(Bm * sz[i]);
+  for (int i = 0; i < ADM_NBUF; ++i) t += (size_t)((Bm * sz[i] + 1) & ~1L);
   return t;
 }
 
@@ -519,6 +519,9 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
     a.active = active;
     a.sol = sol;
     a.sqp_iter = sqp_iter;
+#ifdef I7M_DIAG
+    a.ablate = h->ablate;
+#endif
     // I7M_ADMM_CHUNK = c > 0: the batch as consecutive launches of c problems, so one launch's
     // factors (the blocks every OSQP iteration re-reads) can stay in the 256 MB MALL
     const int chunk = h->admm_chunk > 0 ? std::min(h->admm_chunk, P.B) : P.B;
@@ -535,10 +538,16 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
       });
       if (rc2) return rc2;
       rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
+        // four problems per wave: the launch covers [lo, lo + n) (a.b0 = lo), rows past it idle
+        SolveParams P4 = a.P;
+        P4.B = lo + n;
+        AdmmArgs a4 = a;
+        a4.P = P4;
+        const dim3 g((n + 3) / 4);
         if (a.A.adapt_interval)
-          hipExtLaunchKernelGGL(k_admm_iter<true>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+          hipExtLaunchKernelGGL(k_admm_iter<true>, g, dim3(64), 0, s, ea, eb, 0, a4);
         else
-          hipExtLaunchKernelGGL(k_admm_iter<false>, dim3(n), dim3(64), 0, s, ea, eb, 0, a);
+          hipExtLaunchKernelGGL(k_admm_iter<false>, g, dim3(64), 0, s, ea, eb, 0, a4);
       });
       if (rc2) return rc2;
     }

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <cstdio>
 #include <vector>
 
 namespace {
@@ -908,7 +909,8 @@ struct Solver {
   AdmmParams A_;
   int admm_it = 0, admm_solved = 0;
   // per-stage scaled data (in place, as OSQP's scale_data multiplies its stored matrices)
-  std::vector<double> aPq, aPd, aJ, aI, aqs, als, aD, aE, aLinv, aC;
+  std::vector<double> aPq, aPd, aJ, aI, aqs, als, aD, aE;
+  double rho_cur = 0.1;  // the rho the current factor was built with
   double ac = 1.0;
 
   static double limit_sc(double v) { return v < 1e-4 ? 1.0 : (v > 1e4 ? 1e4 : v); }
@@ -917,7 +919,7 @@ struct Solver {
     const int N = P.N, m = 12 * N;
     aPq.assign(36 * N, 0.0); aPd.assign(T, 0.0); aJ.assign(216 * (N - 1), 0.0); aI.assign(m, 0.0);
     aqs.assign(T, 0.0); als.assign(m, 0.0); aD.assign(T, 1.0); aE.assign(m, 1.0);
-    aLinv.assign(324 * N, 0.0); aC.assign(216 * (N - 1), 0.0);
+    aLinv.assign(324 * N, 0.0);
   }
 
   // unscaled data of the QP at X (after linearize): P blocks, J_k, the -I entries, l; then the
@@ -1040,11 +1042,25 @@ struct Solver {
     }
   }
 
+  // The x-update's matrix M = P_s + sigma I + A_s' rho A_s (every row an equality row here:
+  // rho_vec = 1e3 rho, OSQP's RHO_EQ_OVER_RHO_INEQ) is block tridiagonal: an 18 x 18 block per knot
+  // (x_k, u_k) and the coupling M_{k+1,k} = re diag(I_{k+1}) J_k (x_{k+1} <- z_k).  Its block
+  // Cholesky keeps the inverted diagonal factors Linv_k (S_k = L_k L_k', S_k = M_kk - C_{k-1}
+  // C_{k-1}', C_k = M_{k+1,k} Linv_k'); the solve never needs C, only Linv and J (the device's
+  // stage record: Linv_k packed, J_k compact), as the block LDL' with S_k^-1 = Linv_k' Linv_k:
+  //   forward   g_k = rhs_k - [re I_k (J_{k-1} h_{k-1}); 0],  h_k = Linv_k' (Linv_k g_k)
+  //   backward  xt_k = h_k - Linv_k' (Linv_k (J_k' (re I_{k+1} xt_{k+1}[:12])))
+  // every product an fma chain over its 18 (or 12) terms in ascending order, as the device's
+  // sweeps (indy7_mpc_amd/csrc/i7m_admm.h, k_admm_iter).  (An explicit S_k^-1 instead of the
+  // triangular pair reads the same bytes but lost 5 orders of accuracy on the ill-conditioned M of
+  // a second SQP iteration, cond ~4e7: forward error 1e-5 vs 3e-10)
+  std::vector<double> aLinv;  // (N, 18, 18) Linv_k, zeros above the diagonal and in the last knot's padding
   // block Cholesky of M = P_s + sigma I + A_s' rho A_s; every row is an equality row here
   // (rho_vec = 1e3 rho, OSQP's RHO_EQ_OVER_RHO_INEQ)
   void admm_factor(double rho) {
     const int N = P.N;
     const double re = 1e3 * rho;
+    rho_cur = rho;
     double Cp[12][18];
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
@@ -1094,79 +1110,107 @@ struct Solver {
       if (k < N - 1) {
         // C_k = M_{x_{k+1}, z_k} Linv_k', M_{x_{k+1}, z_k} = re diag(aI_{k+1}) G_k
         const double* G = &aJ[216 * k];
-        double* C = &aC[216 * k];
         for (int a = 0; a < 12; ++a)
           for (int j = 0; j < 18; ++j) {
             double acc = 0.0;
             for (int l = 0; l <= j; ++l) acc += G[18 * a + l] * Li[18 * j + l];
-            C[18 * a + j] = Cp[a][j] = re * aI[12 * (k + 1) + a] * acc;
+            Cp[a][j] = re * aI[12 * (k + 1) + a] * acc;
           }
       }
     }
   }
+  // compact J_k entry (i, j) (the dense 12 x 18 block; the device reads it from its record)
+  double Jkc(int k, int i, int j) const { return aJ[216 * k + 18 * i + j]; }
+  // The device's dot products (indy7_mpc_amd/csrc/i7m_admm.h a4_dot16 / a4_dot6, here adm_dot16 / adm_dot6): 16 terms as four
+  // interleaved fma chains (l mod 4) combined (a0 + a1) + (a2 + a3); 6 terms as two (r even, odd)
+  static double adm_dot16(const double* cf, const double* v) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int l = 0; l < 16; ++l) a[l % 4] = std::fma(cf[l], v[l], a[l % 4]);
+    return (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  static double adm_dot6(const double* cf, const double* v) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int r = 0; r < 6; r += 2) {
+      a0 = std::fma(cf[r], v[r], a0);
+      a1 = std::fma(cf[r + 1], v[r + 1], a1);
+    }
+    return a0 + a1;
+  }
+  // Linv_k (lower) and Linv_k' (upper) times an 18-vector, in the device's order (rows / columns
+  // 0..15 by adm_dot16, then the u-part's terms; the zeros above the diagonal add nothing)
+  void lmul(int k, const double* v, double* o) const {
+    const double* Li = &aLinv[324 * k];
+    for (int c = 0; c < 16; ++c) o[c] = adm_dot16(Li + 18 * c, v);
+    o[16] = std::fma(Li[18 * 16 + 16], v[16], adm_dot16(Li + 18 * 16, v));
+    o[17] = std::fma(Li[18 * 17 + 17], v[17], std::fma(Li[18 * 17 + 16], v[16], adm_dot16(Li + 18 * 17, v)));
+  }
+  void ltmul(int k, const double* v, double* o) const {
+    const double* Li = &aLinv[324 * k];
+    for (int c = 0; c < 16; ++c) {
+      double col[16];
+      for (int l = 0; l < 16; ++l) col[l] = Li[18 * l + c];
+      o[c] = std::fma(Li[18 * 17 + c], v[17], std::fma(Li[18 * 16 + c], v[16], adm_dot16(col, v)));
+    }
+    o[16] = std::fma(Li[18 * 17 + 16], v[17], Li[18 * 16 + 16] * v[16]);
+    o[17] = Li[18 * 17 + 17] * v[17];
+  }
+  // (J_k v)_i, i < 12, in the device's order (the q rows' two entries; the v rows by adm_dot16 + u-part)
+  double Jrow_dot(int k, int i, const double* v) const {
+    if (i < 6) return std::fma(Jkc(k, i, 6 + i), v[6 + i], Jkc(k, i, i) * v[i]);
+    const double* Jr = &aJ[216 * k + 18 * i];
+    return std::fma(Jr[17], v[17], std::fma(Jr[16], v[16], adm_dot16(Jr, v)));
+  }
+  // (J_k' u)_j, j < 18, from init: the q row's entry (column j < 12, zero beyond) with u[j % 6], plus
+  // rows 6..11 (adm_dot6)
+  double Jcol_dot(int k, int j, const double* u, double init) const {
+    const double base = j < 12 ? std::fma(Jkc(k, j % 6, j), u[j % 6], init) : init;
+    double cf[6];
+    for (int r = 0; r < 6; ++r) cf[r] = Jkc(k, 6 + r, j);
+    return base + adm_dot6(cf, u + 6);
+  }
+  // M x = b by the block LDL' above (the device's k_admm_iter solve, without the OSQP steps)
   void admm_solve(const double* b, double* x) const {
     const int N = P.N;
-    double w[64][18];
+    const double re = 1e3 * rho_cur;
+    double h[64][18];
     for (int k = 0; k < N; ++k) {
       const int nk = k < N - 1 ? 18 : 12;
-      double r[18];
-      for (int i = 0; i < nk; ++i) r[i] = b[18 * k + i];
-      if (k > 0) {
-        const double* C = &aC[216 * (k - 1)];
-        for (int a = 0; a < 12; ++a) {
-          double acc = 0.0;
-          for (int j = 0; j < 18; ++j) acc += C[18 * a + j] * w[k - 1][j];
-          r[a] -= acc;
-        }
-      }
-      const double* Li = &aLinv[324 * k];
-      for (int i = 0; i < nk; ++i) {
-        double acc = 0.0;
-        for (int j = 0; j <= i; ++j) acc += Li[18 * i + j] * r[j];
-        w[k][i] = acc;
-      }
+      double g[18], w[18];
+      for (int j = 0; j < 18; ++j) g[j] = j < nk ? b[18 * k + j] : 0.0;
+      if (k > 0)
+        for (int i = 0; i < 12; ++i) g[i] = g[i] - (re * aI[12 * k + i]) * Jrow_dot(k - 1, i, h[k - 1]);
+      lmul(k, g, w);
+      ltmul(k, w, h[k]);
     }
+    double xt[18] = {0.0};
     for (int k = N - 1; k >= 0; --k) {
       const int nk = k < N - 1 ? 18 : 12;
-      double r[18];
-      for (int i = 0; i < nk; ++i) r[i] = w[k][i];
-      if (k < N - 1) {
-        const double* C = &aC[216 * k];
-        for (int j = 0; j < 18; ++j) {
-          double acc = 0.0;
-          for (int a = 0; a < 12; ++a) acc += C[18 * a + j] * x[18 * (k + 1) + a];
-          r[j] -= acc;
-        }
+      double cur[18];
+      if (k == N - 1) {
+        for (int c = 0; c < 18; ++c) cur[c] = h[k][c];
+      } else {
+        double u[12], t[18], s1[18], s2[18];
+        for (int i = 0; i < 12; ++i) u[i] = (re * aI[12 * (k + 1) + i]) * xt[i];
+        for (int j = 0; j < 18; ++j) t[j] = Jcol_dot(k, j, u, 0.0);
+        lmul(k, t, s1);
+        ltmul(k, s1, s2);
+        for (int c = 0; c < 18; ++c) cur[c] = h[k][c] - s2[c];
       }
-      const double* Li = &aLinv[324 * k];
-      for (int j = 0; j < nk; ++j) {
-        double acc = 0.0;
-        for (int i = j; i < nk; ++i) acc += Li[18 * i + j] * r[i];
-        x[18 * k + j] = acc;
-      }
+      for (int c = 0; c < nk; ++c) x[18 * k + c] = cur[c];
+      for (int c = 0; c < 18; ++c) xt[c] = cur[c];
     }
   }
   void admm_Ax(const double* x, double* o) const {
     for (int i = 0; i < 12; ++i) o[i] = aI[i] * x[i];
-    for (int k = 0; k + 1 < P.N; ++k) {
-      const double* G = &aJ[216 * k];
-      for (int i = 0; i < 12; ++i) {
-        double acc = 0.0;
-        for (int j = 0; j < 18; ++j) acc += G[18 * i + j] * x[18 * k + j];
-        o[12 * (k + 1) + i] = acc + aI[12 * (k + 1) + i] * x[18 * (k + 1) + i];
-      }
-    }
+    for (int k = 0; k + 1 < P.N; ++k)
+      for (int i = 0; i < 12; ++i) o[12 * (k + 1) + i] = Jrow_dot(k, i, x + 18 * k) + aI[12 * (k + 1) + i] * x[18 * (k + 1) + i];
   }
   void admm_Aty(const double* t, double* o) const {
     for (int k = 0; k < P.N; ++k) {
       const int nk = k < P.N - 1 ? 18 : 12;
       for (int j = 0; j < nk; ++j) {
-        double acc = j < 12 ? aI[12 * k + j] * t[12 * k + j] : 0.0;
-        if (k < P.N - 1) {
-          const double* G = &aJ[216 * k];
-          for (int i = 0; i < 12; ++i) acc += G[18 * i + j] * t[12 * (k + 1) + i];
-        }
-        o[18 * k + j] = acc;
+        const double init = j < 12 ? aI[12 * k + j] * t[12 * k + j] : 0.0;
+        o[18 * k + j] = k < P.N - 1 ? Jcol_dot(k, j, t + 12 * (k + 1), init) : init;
       }
     }
   }

@@ -73,7 +73,9 @@ def test_port_admm_closed_loop_matches_notebook(trace):
     ends = [rbd.eepos(np.array(q)) for q in trace["endpoint_q"]]
     d = _port_closed_loop(np.array(trace["xstart"]), ends, 16)
     err = np.abs(d - np.array(trace["goal_distances"][:16]))
-    assert err[:3].max() < 1e-13, err
+    # (the block LDL' solve of round 5 reads 1.1e-13 at step 3, the block Cholesky's C form 7e-15:
+    # rounding of the x-update, which the closed loop doubles every ~1.5 steps)
+    assert err[:3].max() < 3e-13, err
     assert err.max() < 1e-9, err
 
 

