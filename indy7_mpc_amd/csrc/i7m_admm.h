@@ -52,6 +52,8 @@ struct AdmmArgs {
   int sqp_iter;
   int b0;      // first problem of this launch (chunked launches: problems [b0, b0 + grid))
   int ablate;  // I7M_DIAG builds only (I7M_ABLATE, timing variants, results invalid); 0 otherwise
+  const double* abase;  // the handle's ADMM allocation (every array above lies in it) and its bytes (< 2 GiB)
+  long abytes;
 };
 
 // HBM layout of the per-stage blocks (what every OSQP iteration streams): the inverted diagonal
@@ -82,13 +84,23 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_ITER_WPE
 #define I7M_ADMM_ITER_WPE 2  // ... and k_admm_iter without adaptive rho (at 3: 78 spilled VGPRs, 30% slower)
 #endif
-constexpr int ADM_LP = 171, ADM_JC = 120;
-// One record per stage, N per problem (problem b's at R + b N ADM_REC): [Linv_k packed lower
-// (171) | compact J_k (120) | pad (1)] = 292 doubles, 16-byte aligned.  k_admm_iter streams it
-// twice per OSQP iteration (forward and backward sweep); the coupling C_k = M_{k+1,k} Linv_k' of
-// the factor is never stored: the sweeps apply it as re I_{k+1} J_k and the triangular pair.
-constexpr int ADM_REC = 292, REC_J = ADM_LP;
-__device__ __forceinline__ int adm_tri(int i, int j) { return i * (i + 1) / 2 + j; }
+constexpr int ADM_LP = 196, ADM_JC = 120;
+// One record per stage, N per problem (problem b's at R + b N ADM_REC): [Linv_k | compact J_k]
+// = 316 doubles (158 pieces of 16 B).  Linv_k's rows 0-15 are stored lower-triangular with each
+// row padded with zeros to a multiple of four entries (widths 4, 8, 12, 16: 160 doubles), rows 16
+// and 17 in full (36): every lane's row and column reads in k_admm_iter are then a base plus a
+// constant, and the entries past a padded row are never read (the DPP fma's bank masks skip
+// them).  k_admm_iter streams the record twice per OSQP iteration (forward and backward sweep);
+// the coupling C_k = M_{k+1,k} Linv_k' of the factor is never stored: the sweeps apply it as
+// re I_{k+1} J_k and the triangular pair.
+constexpr int ADM_REC = 316, REC_J = ADM_LP;
+// entry (i, j) of Linv_k in the record, and the stored width of row i
+__device__ __forceinline__ int adm_lw(int i) { return i < 16 ? 4 * (i / 4 + 1) : 18; }
+__device__ __forceinline__ int adm_lrow(int i) {
+  const int g = i >> 2;
+  return i < 16 ? 8 * g * (g + 1) + 4 * (g + 1) * (i - 4 * g) : 160 + 18 * (i - 16);
+}
+__device__ __forceinline__ int adm_lrec(int i, int j) { return adm_lrow(i) + j; }
 // dense 12 x 18 J_k into LDS from its compact form
 __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
   for (int e = l; e < 216; e += 64) {
@@ -519,7 +531,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       for (int i = 0; i < 18; ++i) {
         const double v = i < nk && l < nk ? x[i] : 0.0;
         sL[18 * i + l] = v;
-        if (i >= l) Rb[ADM_REC * k + adm_tri(i, l)] = v;
+        if (l < adm_lw(i)) Rb[ADM_REC * k + adm_lrec(i, l)] = v;  // (+0 above the diagonal)
       }
     }
     wave_sync();
@@ -600,7 +612,7 @@ __device__ void adm_factor_lds(const AdmmArgs& a, int N, double rho, const doubl
     wave_sync();
     for (int e = l; e < 324; e += 64) {
       const int i = e / 18, j = e - 18 * i;
-      if (j <= i) Rb[ADM_REC * k + adm_tri(i, j)] = sL[e];
+      if (j < adm_lw(i)) Rb[ADM_REC * k + adm_lrec(i, j)] = sL[e];
     }
     if (k < N - 1) {
       for (int e = l; e < 216; e += 64) {
@@ -664,15 +676,26 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
 //   backward  xt_k = h_k - Linv_k' (Linv_k (J_k' (re I_{k+1} xt_{k+1}[:12])))
 // then z~ = J_k xt_k + I_{k+1} xt_{k+1} for block k+1's rows, OSQP's relaxation, projection and dual
 // update.  Every mat-vec is a chain of fma's whose broadcast operand comes from the row's own lanes
-// by DPP (v_mov_b64_dpp row_newbcast: no LDS round trip on the sweep's chain); the matrix operand
-// is read from the stage's LDS image.  Each step's stage record (Linv packed | compact J: 292
-// doubles per problem, 10 dwordx4 per lane) is loaded two steps ahead into registers, then
-// scattered into a dense LDS image (Linv 18 x 18, J 12 x 18, zeros fixed) at the step's start; the
-// step's vectors ride in the same ring.  Problems stop at their own termination test; a finished
-// row keeps shadowing the others' loads (its addresses are a running row's) and stores nothing.
-constexpr int A4_PS = 541;  // doubles of one problem's LDS image (Linv 324 | J 216 | zero); odd:
-                            // two problems of a lane half read disjoint banks
-constexpr int A4_LJ = 324;
+// by DPP (v_fmac_f64_dpp row_newbcast: no LDS round trip on the sweep's chain); the matrix operand
+// is read from LDS, straight out of the stage record as HBM holds it (ADM_REC's padded rows make
+// every read a base plus a constant).
+//
+// Every byte the sweeps read arrives by LDS DMA (buffer_load_dwordx4 ... lds): a step's four stage
+// records (10 wave-instructions) and its vectors (3) land in one slot of a three-slot ring two steps
+// before the step, so no register holds data in flight (a register ring costs 120 VGPRs, and a
+// spilled or copied member waits for its load) and the wave's only waits on memory are one counted
+// s_waitcnt vmcnt per step.  The DMA is issued from inline asm, so the compiler neither sees it nor
+// drains it at its own waits; the ring's LDS reads are ordinary (compiler-scheduled) reads behind
+// the asm's memory clobber.  All arrays are reached through one buffer resource over the handle's
+// ADMM allocation (32-bit byte offsets; out-of-range offsets read zeros and drop stores, which
+// masks finished and absent rows without branches).  Problems stop at their own termination test.
+constexpr int A5_RI = 10;                      // record DMA wave-instructions per step (640 >= 4 x 158 pieces)
+constexpr int A5_VI = 3;                       // vector DMA wave-instructions per step (192 >= 4 x 42 pieces)
+constexpr int A5_SLOT = 64 * (A5_RI + A5_VI);  // 16-B pieces per ring slot (13 KB)
+constexpr int A5_VP = 42;                      // vector pieces per problem and step
+constexpr int A5_RP = ADM_REC / 2;             // record pieces per problem and stage (158)
+constexpr int A5_VD = 2 * 64 * A5_RI;          // the slot's vector part (doubles)
+constexpr unsigned A5_OOB = 0x7ff00000u;       // a byte offset past every allocation (< 2 GiB enforced by the host)
 template <int n>
 __device__ __forceinline__ double a4_bc(double v) {  // lane n of the 16-lane row, to every lane of it
   return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + n, 0xf, 0xf, false);
@@ -705,17 +728,18 @@ struct A4Vec {
 // acc += (lane n of the row's v) * coef: v_fmac_f64_dpp with the broadcast fused (DP DPP takes only
 // row_newbcast).  Four fma's per statement into four accumulators; the statement opens with the
 // two wait states a DPP read of a VGPR a VALU just wrote needs (the compiler pads no asm).
-template <int n>
+// BM: the lanes written (bank b = lanes 4b..4b+3 of every row); the masked lanes keep their sums
+template <int n, int BM = 0xf>
 __device__ __forceinline__ void a4_fmac4(double& a0, double& a1, double& a2, double& a3, double v, double c0, double c1,
                                          double c2, double c3) {
   asm volatile(
       "s_nop 1\n\t"
-      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:%9 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %4, %6 row_newbcast:%10 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %2, %4, %7 row_newbcast:%11 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %3, %4, %8 row_newbcast:%12 row_mask:0xf bank_mask:0xf"
+      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:%9 row_mask:0xf bank_mask:%13\n\t"
+      "v_fmac_f64_dpp %1, %4, %6 row_newbcast:%10 row_mask:0xf bank_mask:%13\n\t"
+      "v_fmac_f64_dpp %2, %4, %7 row_newbcast:%11 row_mask:0xf bank_mask:%13\n\t"
+      "v_fmac_f64_dpp %3, %4, %8 row_newbcast:%12 row_mask:0xf bank_mask:%13"
       : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
-      : "v"(v), "v"(c0), "v"(c1), "v"(c2), "v"(c3), "i"(n), "i"(n + 1), "i"(n + 2), "i"(n + 3));
+      : "v"(v), "v"(c0), "v"(c1), "v"(c2), "v"(c3), "i"(n), "i"(n + 1), "i"(n + 2), "i"(n + 3), "i"(BM));
 }
 template <int n>
 __device__ __forceinline__ void a4_fmac2(double& a0, double& a1, double v, double c0, double c1) {
@@ -727,13 +751,18 @@ __device__ __forceinline__ void a4_fmac2(double& a0, double& a1, double v, doubl
       : "v"(v), "v"(c0), "v"(c1), "i"(n), "i"(n + 1));
 }
 // sum_{l < 16} coef[l] * v_l as four interleaved chains (l mod 4), combined (a0 + a1) + (a2 + a3):
-// the device's and the port's order (oracle/cpp/i7m_cpu.cpp dot16)
+// the device's and the port's order (oracle/cpp/i7m_cpu.cpp adm_dot16).  TRI 1: lane c takes
+// terms l <= c only (a lower-triangular row: the terms of a group of four past lane c's bank are
+// masked, those inside it read the row's zero padding); TRI 2: terms l >= c only (a column).
+template <int TRI = 0>
 __device__ __forceinline__ double a4_dot16(double v, const double* cf) {
+  constexpr int M0 = TRI == 1 ? 0xf : TRI == 2 ? 0x1 : 0xf, M1 = TRI == 1 ? 0xe : TRI == 2 ? 0x3 : 0xf;
+  constexpr int M2 = TRI == 1 ? 0xc : TRI == 2 ? 0x7 : 0xf, M3 = TRI == 1 ? 0x8 : 0xf;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  a4_fmac4<0>(a0, a1, a2, a3, v, cf[0], cf[1], cf[2], cf[3]);
-  a4_fmac4<4>(a0, a1, a2, a3, v, cf[4], cf[5], cf[6], cf[7]);
-  a4_fmac4<8>(a0, a1, a2, a3, v, cf[8], cf[9], cf[10], cf[11]);
-  a4_fmac4<12>(a0, a1, a2, a3, v, cf[12], cf[13], cf[14], cf[15]);
+  a4_fmac4<0, M0>(a0, a1, a2, a3, v, cf[0], cf[1], cf[2], cf[3]);
+  a4_fmac4<4, M1>(a0, a1, a2, a3, v, cf[4], cf[5], cf[6], cf[7]);
+  a4_fmac4<8, M2>(a0, a1, a2, a3, v, cf[8], cf[9], cf[10], cf[11]);
+  a4_fmac4<12, M3>(a0, a1, a2, a3, v, cf[12], cf[13], cf[14], cf[15]);
   return __dadd_rn(__dadd_rn(a0, a1), __dadd_rn(a2, a3));
 }
 // sum_{r = 6..11} coef[r - 6] * u_r as two chains (r even / odd), combined
@@ -744,69 +773,98 @@ __device__ __forceinline__ double a4_dot6(double u, const double* cf) {
   a4_fmac2<10>(a0, a1, u, cf[4], cf[5]);
   return __dadd_rn(a0, a1);
 }
-// One stage image's coefficients of a lane, read from LDS at the step's start (all reads issued
-// before the first fma: one LDS latency per step, not one per chain)
-struct A4Coef {
-  double L[16], L16[17], L17[18];   // Linv row c, rows 16 and 17 (lmul)
-  double Lt[16], Lt16c, Lt17c;      // Linv column c (l < 16), L[16][c], L[17][c] (ltmul)
-  double l1616, l1716, l1717;       // the (16, 17) block (ltmul)
-  double Jt[6], J16[6], J17[6], Jd; // J column c (rows 6..11), columns 16, 17 (rows 6..11), J[c % 6][c] (jtmul)
-  double Jr[18], Jq0, Jq1;          // J row c (c in 6..11; row 11 above), J[q][q], J[q][6 + q] (jmul, q = c < 6 ? c : 0)
+// sum over the row's 16 lanes of cf_c v_c (a pairwise tree: lane 15 gathers lanes 14, 12-13, 8-11,
+// 0-7 by row_shr 1, 2, 4, 8; the first level fma(cf_c, v_c, p_{c-1})), broadcast to the row: the
+// port's adm_rowsum order.  (bound_ctrl: lanes below the shift read 0; only lane 15 is kept)
+template <int n>
+__device__ __forceinline__ double a4_shr(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, 0x110 + n, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x110 + n, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double a4_rowsum(double cf, double v) {
+  double p = __fma_rn(cf, v, a4_shr<1>(__dmul_rn(cf, v)));
+  p = __dadd_rn(p, a4_shr<2>(p));
+  p = __dadd_rn(p, a4_shr<4>(p));
+  p = __dadd_rn(p, a4_shr<8>(p));
+  return a4_bc<15>(p);
+}
+// A stage's coefficients, read from the ring slot in four sets, each just before the phase ahead
+// of the one that uses it (the reads stay where they are written: the fma asm is volatile).  R is
+// the problem's record in the slot.
+struct A4CJ {
+  double Jt[6], J16[6], J17[6], Jd;  // J column c (rows 6..11), columns 16, 17 (rows 6..11), J[c % 6][c]
 };
-__device__ __forceinline__ void a4_coef(A4Coef& C, const double* Lb, int c) {
-  const double* Jb = Lb + A4_LJ;
-#pragma unroll
-  for (int l = 0; l < 16; ++l) C.L[l] = Lb[18 * c + l];
-#pragma unroll
-  for (int l = 0; l < 17; ++l) C.L16[l] = Lb[18 * 16 + l];
-#pragma unroll
-  for (int l = 0; l < 18; ++l) C.L17[l] = Lb[18 * 17 + l];
-#pragma unroll
-  for (int l = 0; l < 16; ++l) C.Lt[l] = Lb[18 * l + c];
-  C.Lt16c = Lb[18 * 16 + c];
-  C.Lt17c = Lb[18 * 17 + c];
-  C.l1616 = Lb[18 * 16 + 16];
-  C.l1716 = Lb[18 * 17 + 16];
-  C.l1717 = Lb[18 * 17 + 17];
+struct A4CL {
+  double L[16];          // Linv row c (l < 16; the entries past the padded row are never used)
+  double Lc16, Lc17;     // Linv[16][c], Linv[17][c]
+  double d66, d76, d77;  // Linv[16][16], Linv[17][16], Linv[17][17]
+};
+struct A4CT {
+  double Lt[16];  // Linv column c (rows l < 16; rows whose padded width ends before c are never used)
+};
+struct A4CR {
+  double Jr[18], Jq0, Jq1;  // J row c (v rows 6..11; clamped outside them), J[q][q], J[q][6 + q] (q = c < 6 ? c : 0)
+};
+__device__ __forceinline__ void a4_ldj(A4CJ& C, const double* R, int c) {
+  const double* J = R + REC_J;  // [J[i][i] (6) | J[i][6 + i] (6) | v rows 6 x 18]
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    C.Jt[r] = Jb[18 * (6 + r) + c];
-    C.J16[r] = Jb[18 * (6 + r) + 16];
-    C.J17[r] = Jb[18 * (6 + r) + 17];
+    C.Jt[r] = J[12 + 18 * r + c];
+    C.J16[r] = J[12 + 18 * r + 16];
+    C.J17[r] = J[12 + 18 * r + 17];
   }
-  C.Jd = Jb[18 * (c % 6) + c];
-  const int rr = c < 12 ? c : 11;
-#pragma unroll
-  for (int l = 0; l < 18; ++l) C.Jr[l] = Jb[18 * rr + l];
-  const int q = c < 6 ? c : 0;
-  C.Jq0 = Jb[18 * q + q];
-  C.Jq1 = Jb[18 * q + 6 + q];
+  C.Jd = c < 12 ? J[c] : 0.0;
 }
-// y = Linv v
-__device__ __forceinline__ A4Vec a4_lmul(const A4Coef& C, const A4Vec& v) {
-  const double lo = a4_dot16(v.lo, C.L);
-  double b16 = a4_dot16(v.lo, C.L16), b17 = a4_dot16(v.lo, C.L17);
-  b16 = __fma_rn(C.L16[16], v.h16, b16);
-  b17 = __fma_rn(C.L17[16], v.h16, b17);
-  b17 = __fma_rn(C.L17[17], v.h17, b17);
+__device__ __forceinline__ void a4_ldl(A4CL& C, const double* R, const double* Rrow, int c) {
+#pragma unroll
+  for (int l = 0; l < 16; ++l) C.L[l] = Rrow[l];
+  C.Lc16 = R[160 + c];
+  C.Lc17 = R[178 + c];
+  C.d66 = R[176];
+  C.d76 = R[194];
+  C.d77 = R[195];
+}
+// row l's entry c: R + adm_lrow(l) + c (adm_lrow a constant per l)
+__device__ __forceinline__ void a4_ldt(A4CT& C, const double* R, int c) {
+  constexpr int rs[16] = {0, 4, 8, 12, 16, 24, 32, 40, 48, 60, 72, 84, 96, 112, 128, 144};
+#pragma unroll
+  for (int l = 0; l < 16; ++l) C.Lt[l] = R[rs[l] + c];
+}
+__device__ __forceinline__ void a4_ldr(A4CR& C, const double* R, int c) {
+  const double* J = R + REC_J;
+  const int rr = c < 6 ? 0 : (c < 12 ? c - 6 : 5);
+#pragma unroll
+  for (int l = 0; l < 18; ++l) C.Jr[l] = J[12 + 18 * rr + l];
+  const int q = c < 6 ? c : 0;
+  C.Jq0 = J[q];
+  C.Jq1 = J[6 + q];
+}
+// y = Linv v (rows 16, 17: the row sums of Linv[16 or 17][c] v_c, then the (16, 17) block)
+__device__ __forceinline__ A4Vec a4_lmul(const A4CL& C, const A4Vec& v) {
+  const double lo = a4_dot16<1>(v.lo, C.L);
+  const double s16 = a4_rowsum(C.Lc16, v.lo), s17 = a4_rowsum(C.Lc17, v.lo);
+  const double b16 = __fma_rn(C.d66, v.h16, s16);
+  const double b17 = __fma_rn(C.d77, v.h17, __fma_rn(C.d76, v.h16, s17));
   return {lo, b16, b17};
 }
 // y = Linv' v
-__device__ __forceinline__ A4Vec a4_ltmul(const A4Coef& C, const A4Vec& v) {
-  double lo = a4_dot16(v.lo, C.Lt);
-  lo = __fma_rn(C.Lt16c, v.h16, lo);
-  lo = __fma_rn(C.Lt17c, v.h17, lo);
-  return {lo, __fma_rn(C.l1716, v.h17, __dmul_rn(C.l1616, v.h16)), __dmul_rn(C.l1717, v.h17)};
+__device__ __forceinline__ A4Vec a4_ltmul(const A4CL& L, const A4CT& C, const A4Vec& v) {
+  double lo = a4_dot16<2>(v.lo, C.Lt);
+  lo = __fma_rn(L.Lc16, v.h16, lo);
+  lo = __fma_rn(L.Lc17, v.h17, lo);
+  return {lo, __fma_rn(L.d76, v.h17, __dmul_rn(L.d66, v.h16)), __dmul_rn(L.d77, v.h17)};
 }
 // init + J' u: the q-row entry of column c (J[c % 6][c], zero for c >= 12) with u[c % 6], plus the
 // v rows 6..11 (two chains); u in lanes 0..11, every lane's finite
-__device__ __forceinline__ A4Vec a4_jtmul(const A4Coef& C, double u, A4Vec init) {
+__device__ __forceinline__ A4Vec a4_jtmul(const A4CJ& C, double u, A4Vec init) {
   const double us = a4_shr6(u);  // u[c - 6] for c >= 6, own below
   const double lo = __dadd_rn(__fma_rn(C.Jd, us, init.lo), a4_dot6(u, C.Jt));
   return {lo, __dadd_rn(init.h16, a4_dot6(u, C.J16)), __dadd_rn(init.h17, a4_dot6(u, C.J17))};
 }
 // (J v)_c, c < 12 (lanes 12-15: row 11's, unused)
-__device__ __forceinline__ double a4_jmul(const A4Coef& C, int c, const A4Vec& v) {
+__device__ __forceinline__ double a4_jmul(const A4CR& C, int c, const A4Vec& v) {
   double a = a4_dot16(v.lo, C.Jr);
   a = __fma_rn(C.Jr[16], v.h16, a);
   a = __fma_rn(C.Jr[17], v.h17, a);
@@ -814,188 +872,209 @@ __device__ __forceinline__ double a4_jmul(const A4Coef& C, int c, const A4Vec& v
   return c < 6 ? sp : a;
 }
 
-// The ring buffer of one step: the stage record (this lane's 10 chunks) and the step's vectors.
-struct A4Buf {
-  double2 rec[10];  // chunks c + 16 t of the lane's problem's stage record
-  double v0, v1, z1, y1, l1, ib1;
-  double2 hv0, hv1;
-};
-
-// Buffer-resource access (uniform base in SGPRs, 32-bit per-lane offset, hardware range check): a
-// store or load at an offset past the range does nothing (loads return 0), which masks the stores
-// of finished rows and of absent rows without branches.
 typedef unsigned int a4u2 __attribute__((ext_vector_type(2)));
-typedef unsigned int a4u4 __attribute__((ext_vector_type(4)));
-constexpr int A4_OOB = 1 << 27;  // doubles: beyond every range
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t a4_rsrc(const void* base, long bytes) {
   const unsigned long long u = (unsigned long long)base;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
   const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
 }
-__device__ __forceinline__ double a4_ld(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off * 8, 0, 0));
+__device__ __forceinline__ double a5_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
-__device__ __forceinline__ double2 a4_ld2(__amdgpu_buffer_rsrc_t r, int off) {
-  const a4u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off * 8, 0, 0);
-  return make_double2(__builtin_bit_cast(double, a4u2{v.x, v.y}), __builtin_bit_cast(double, a4u2{v.z, v.w}));
+__device__ __forceinline__ void a5_st(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(a4u2, v), r, off, 0, 0);
 }
-__device__ __forceinline__ void a4_st(double v, __amdgpu_buffer_rsrc_t r, int off) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(a4u2, v), r, off * 8, 0, 0);
+// one step's DMA: 10 record wave-instructions (per-lane offsets ro[t], the stage in soffset) and 3
+// vector ones (per-lane offsets vo[u]), to the slot at LDS byte address `lds` (M0 = the
+// wave-instruction's 1 KB, saved and restored around)
+__device__ __forceinline__ void a5_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, const unsigned (&ro)[A5_RI], unsigned so,
+                                       const unsigned (&vo)[A5_VI]) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %7, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %8, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %9, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %10, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %11, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %12, %15, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %13, %15, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %14, %15, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "v"(ro[0]), "v"(ro[1]), "v"(ro[2]), "v"(ro[3]), "v"(ro[4]), "v"(ro[5]), "v"(ro[6]), "v"(ro[7]),
+        "v"(ro[8]), "v"(ro[9]), "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(r), "s"(so)
+      : "memory");
 }
+// the step's slot has landed: at most 13 vector-memory operations in flight (the next step's DMA,
+// or the stores issued after its first ones: every operation completes in issue order)
+__device__ __forceinline__ void a5_wait() { asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); }
+__device__ __forceinline__ void a5_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// OSQP's iteration loop of one wave (four problems).  Per-lane state lives in registers; the
-// arrays are per-wave buffer resources (SGPRs) with small per-lane offsets.
+// OSQP's iteration loop of one wave (four problems).  Per-lane state lives in registers.
 template <bool ADAPT>
 __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   const SolveParams& P = a.P;
   const int N = P.N, T = P.T, m = 12 * N;
   const int l = threadIdx.x, p = l >> 4, c = l & 15;
-  __shared__ double sImg[4 * A4_PS];
-  double* Lb = sImg + A4_PS * p;  // this problem's stage image: Linv dense (18 x 18), J dense at +324
+  __shared__ double2 sRing[3 * A5_SLOT];
+  double* const ring = (double*)sRing;
+  const unsigned ring_lds = (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)sRing;
   const int bb = a.b0 + 4 * (int)blockIdx.x;
   bool run = bb + p < P.B && !(a.active && !a.active[bb + p]);
   const bool act = run;
   if (!__ballot(run)) return;
-  // the wave's four problems' rows of every array
-  const long wT = (long)bb * T, wm = (long)bb * m, wR = (long)bb * N * ADM_REC;
-  const auto rX = a4_rsrc(a.sx + wT, 32L * T), rZ = a4_rsrc(a.sz + wm, 32L * m), rY = a4_rsrc(a.sy + wm, 32L * m);
-  const auto rQ = a4_rsrc(a.qs + wT, 32L * T), rL = a4_rsrc(a.ls + wm, 32L * m), rI = a4_rsrc(a.I + wm, 32L * m);
-  const auto rH = a4_rsrc(a.w + wT, 32L * T), rR = a4_rsrc(a.R + wR, 32L * N * ADM_REC);
-  int prow = p;  // the row whose problem this lane's loads read (a finished or idle row reads a running one's)
-  auto pick_shadow = [&]() {
-    const unsigned long long any = __ballot(run);
-    if (any && !run) prow = (__ffsll((long long)any) - 1) >> 4;
-  };
-  pick_shadow();
-  int oT = prow * T, om = prow * m, oR = prow * N * ADM_REC;
   const int bown = bb + p;
-  const double c_cost = a.cs[bb + prow];
-  double rho = a.srho[bb + prow];
+  // one resource over the whole allocation; every array as a byte offset in it
+  const auto rA = a4_rsrc(a.abase, a.abytes);
+  auto boff = [&](const double* q) { return (unsigned)__builtin_amdgcn_readfirstlane((int)((const char*)q - (const char*)a.abase)); };
+  const unsigned oX = boff(a.sx), oZ = boff(a.sz), oY = boff(a.sy), oQ = boff(a.qs), oL = boff(a.ls), oI = boff(a.I);
+  const unsigned oH = boff(a.w), oR = boff(a.R);
+  // this lane's own rows (stores, the block-0 epilogue)
+  const unsigned xT = oX + 8u * (unsigned)(bown * T), hT = oH + 8u * (unsigned)(bown * T);
+  const unsigned zM = oZ + 8u * (unsigned)(bown * m), yM = oY + 8u * (unsigned)(bown * m);
+  const unsigned lM = oL + 8u * (unsigned)(bown * m), iM = oI + 8u * (unsigned)(bown * m);
+  const double c_cost = a.cs[bown < P.B ? bown : bb];
+  double rho = a.srho[bown < P.B ? bown : bb];
   double rv = 1e3 * rho, ri = 1.0 / rv;
   const double al = a.A.alpha, sg = a.A.sigma, al1 = 1.0 - al;
-  for (int e = l; e < 4 * A4_PS; e += 64) sImg[e] = 0.0;
-  // this lane's chunk destinations in the image (packed Linv -> 18 i + j, compact J -> 324 + 18 i + j)
-  int dst[10];
-#pragma unroll
-  for (int t = 0; t < 10; ++t) {
-    int code = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int e = 2 * (c + 16 * t) + h;
-      if (e > ADM_REC - 1) e = ADM_REC - 1;
-      int d;
-      if (e < ADM_LP) {
-        int i = 0;
-        while ((i + 1) * (i + 2) / 2 <= e) ++i;
-        d = 18 * i + (e - i * (i + 1) / 2);
-      } else if (e < ADM_LP + ADM_JC) {
-        const int q = e - ADM_LP;
-        if (q < 6) d = A4_LJ + 19 * q;
-        else if (q < 12) d = A4_LJ + 18 * (q - 6) + q;
-        else d = A4_LJ + 18 * (6 + (q - 12) / 18) + (q - 12) % 18;
-      } else {
-        d = A4_PS - 1;
-      }
-      code |= d << (16 * h);
-    }
-    dst[t] = code;
-  }
   const int cc = c < 12 ? c : 11;
   const int c16 = 16 + (c & 1);  // lanes 0, 1 store the u-part pair (16, 17)
   const bool lo12 = c < 12, lo2 = c < 2;
-  int chk_off[10];
+  // DMA source offsets of this lane's pieces (rows that do not run read nothing: out of range).
+  // Records: piece g = 64 t + l of the four problems' 632; vectors: piece g = 64 u + l of their
+  // 168, problem g / 42 piece j = g % 42: [0, 9) v0, [9, 18) v1, [18, 42) z, y, l, I (6 each).
+  unsigned ro[A5_RI], vF[A5_VI], vB[A5_VI];
+  int vcls[A5_VI];
+  auto offsets = [&]() {
+    const unsigned long long rm = __ballot(run);
 #pragma unroll
-  for (int t = 0; t < 10; ++t) chk_off[t] = 2 * ((c + 16 * t) < 146 ? c + 16 * t : 145);
-  // the loads of step s (< 2N) of an iteration: its stage record; forward: x_k, q_k; backward: h_k,
-  // x_{k+1}; both: block k+1's z, y, l, I.  Every index in bounds (the last stage's missing rows
-  // and u-parts read a neighbour, unused).
-  auto issue = [&](A4Buf& B, int s) {
+    for (int t = 0; t < A5_RI; ++t) {
+      const int g = 64 * t + l, q = g / A5_RP, j = g - A5_RP * q;
+      const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
+      ro[t] = ok ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * j : A5_OOB;
+    }
+#pragma unroll
+    for (int u = 0; u < A5_VI; ++u) {
+      const int g = 64 * u + l, q = g / A5_VP, j = g - A5_VP * q;
+      const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
+      const unsigned rT = 8u * (unsigned)((bb + q) * T), rM = 8u * (unsigned)((bb + q) * m);
+      unsigned f, bk;
+      int cl;
+      if (j < 9) {
+        f = oX + rT + 16u * j; bk = oH + rT + 16u * j; cl = 0;
+      } else if (j < 18) {
+        f = oQ + rT + 16u * (j - 9); bk = oX + rT + 16u * (j - 9); cl = 1;
+      } else {
+        const int jj = j - 18, w = jj / 6;
+        f = (w == 0 ? oZ + 0u : w == 1 ? oY + 0u : w == 2 ? oL + 0u : oI + 0u) + rM + 16u * (jj - 6 * w);
+        bk = f; cl = 2;
+      }
+      vF[u] = ok ? f : A5_OOB;
+      vB[u] = ok ? bk : A5_OOB;
+      vcls[u] = cl;
+    }
+  };
+  offsets();
+  // issue step s's DMA (s < 2N) into ring slot `slot`: its stage record; forward: x_k, q_k;
+  // backward: h_k, x_{k+1}; both: block k+1's z, y, l, I (the last stage's missing block reads
+  // block N-1's, unused)
+  auto issue = [&](int s, int slot) {
     const bool fwd = s < N;
     const int k = fwd ? s : 2 * N - 1 - s;
     const int k1 = k + 1 < N ? k + 1 : N - 1;
-    const int kh = k < N - 1 ? k : N - 2;
+    const int kb = fwd ? k : k1;
 #ifdef I7M_DIAG
     // I7M_ABLATE 21: every step reads stage 0's record (L2-resident: the sweep without its stream)
-    const int ro = oR + (a.ablate == 21 ? 0 : k * ADM_REC);
+    const unsigned so = 8u * (unsigned)(a.ablate == 21 ? 0 : k * ADM_REC);
 #else
-    const int ro = oR + k * ADM_REC;
+    const unsigned so = 8u * (unsigned)(k * ADM_REC);
 #endif
+    unsigned vo[A5_VI];
 #pragma unroll
-    for (int t = 0; t < 10; ++t) B.rec[t] = a4_ld2(rR, ro + chk_off[t]);
-    const int ci = k < N - 1 ? c : cc;
-    const int kb = fwd ? k : k1;  // the stage of v1
-    const int kbh = kb < N - 1 ? kb : N - 2;
-    const int cb = kb < N - 1 ? c : cc;
-    if (fwd) {
-      B.v0 = a4_ld(rX, oT + 18 * k + ci);
-      B.v1 = a4_ld(rQ, oT + 18 * kb + cb);
-      B.hv0 = a4_ld2(rX, oT + 18 * kh + 16);
-      B.hv1 = a4_ld2(rQ, oT + 18 * kbh + 16);
-    } else {
-      B.v0 = a4_ld(rH, oT + 18 * k + ci);
-      B.v1 = a4_ld(rX, oT + 18 * kb + cb);
-      B.hv0 = a4_ld2(rH, oT + 18 * kh + 16);
-      B.hv1 = a4_ld2(rX, oT + 18 * kbh + 16);
+    for (int u = 0; u < A5_VI; ++u) {
+      const unsigned st = vcls[u] == 0 ? 144u * k : (vcls[u] == 1 ? 144u * kb : 96u * k1);
+      vo[u] = (fwd ? vF[u] + 0u : vB[u] + 0u) + st;
     }
-    const int ob = om + 12 * k1 + cc;
-    B.z1 = a4_ld(rZ, ob);
-    B.y1 = a4_ld(rY, ob);
-    B.l1 = a4_ld(rL, ob);
-    B.ib1 = a4_ld(rI, ob);
+    a5_dma(rA, ring_lds + 16u * A5_SLOT * slot, ro, so, vo);
   };
-  auto scatter = [&](const A4Buf& B) {
-#pragma unroll
-    for (int t = 0; t < 10; ++t) {
-      Lb[dst[t] & 0xffff] = B.rec[t].x;
-      Lb[dst[t] >> 16] = B.rec[t].y;
-    }
-  };
-  A4Buf A0, A1;
-  issue(A0, 0);
-  issue(A1, 1);
+  issue(0, 0);
+  issue(1, 1);
   // carried between steps
   A4Vec hc{0.0, 0.0, 0.0};  // forward: J_{k-1} h_{k-1} (lanes 0..11) / backward: xt_{k+1}
-  double tk = __dmul_rn(rv, __dsub_rn(a4_ld(rZ, om + cc), __dmul_rn(ri, a4_ld(rY, om + cc))));  // block k's t
-  double ibk = a4_ld(rI, om + cc);
-  // the state the backward sweep hands to the next forward sweep's first two steps (their memory
-  // copies were loaded before the backward sweep wrote them)
+  double tk = __dmul_rn(rv, __dsub_rn(a5_ld(rA, zM + 8 * cc), __dmul_rn(ri, a5_ld(rA, yM + 8 * cc))));  // block k's t
+  double ibk = a5_ld(rA, iM + 8 * cc);
+  // the state the backward sweep hands to the next forward sweep's first two steps (their DMA was
+  // issued before the backward sweep wrote them)
   double nx0 = 0.0, nx1 = 0.0, nz1 = 0.0, ny1 = 0.0;
   double2 nx0h = make_double2(0.0, 0.0), nx1h = make_double2(0.0, 0.0);
   int done_it = 0;
   bool solved = false;
-  // one step's start: the record into the image, the step's vectors out of the ring, the ring
-  // advanced and the load of step s + 2 issued
   double v0, v1, z1, y1, l1, ib1;
   double2 hv0, hv1;
-  A4Coef C;
-  auto begin = [&](int s) {
-    __asm__ volatile("" ::: "memory");
-    scatter(A0);
-    __asm__ volatile("" ::: "memory");
-    a4_coef(C, Lb, c);
-    v0 = A0.v0; v1 = A0.v1; z1 = A0.z1; y1 = A0.y1; l1 = A0.l1; ib1 = A0.ib1; hv0 = A0.hv0; hv1 = A0.hv1;
-    A0 = A1;
-    int sn = s + 2;
+  A4CJ CJ;
+  A4CL CL;
+  A4CT CT;
+  A4CR CR;
+  const double* R = nullptr;
+  // one step's start: wait for its slot, issue step s + 2's DMA into the slot step s - 1 used, read
+  // the step's vectors and the first two coefficient sets
+  auto begin = [&](int s, int slot) {
+    a5_wait();
+    int sn = s + 2, sl = slot + 2;
     if (sn >= 2 * N) sn -= 2 * N;
-    issue(A1, sn);
+    if (sl >= 3) sl -= 3;
+    issue(sn, sl);
+    const double* S = ring + 2 * A5_SLOT * slot;
+    R = S + ADM_REC * p;
+    const double* V = S + A5_VD + 2 * A5_VP * p;  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
+    const bool last = s == N - 1 || s == N;       // stage N-1: 12 rows
+    // (prvalue selects: a conditional of two captured lvalues becomes a select of their addresses
+    // and a memory load, which waits for every DMA in flight)
+    const int ci = last ? (c < 12 ? c : 11) : c + 0;
+    const int cb = s == N - 1 || s == N || s == N + 1 ? (c < 12 ? c : 11) : c + 0;
+    v0 = V[ci];
+    v1 = V[18 + cb];
+    hv0 = make_double2(V[16], V[17]);
+    hv1 = make_double2(V[34], V[35]);
+    z1 = V[36 + cc];
+    y1 = V[48 + cc];
+    l1 = V[60 + cc];
+    ib1 = V[72 + cc];
+    a4_ldj(CJ, R, c);
+    a4_ldl(CL, R, R + adm_lrow(c), c);
   };
   // store offsets: masked (past the range) for rows that do not run
-  auto so = [&](bool ok, int off) { return run && ok ? off : A4_OOB; };
+  auto so = [&](bool ok, unsigned off) { return run && ok ? off + 0u : A5_OOB + 0u; };
+  // Linv' Linv r, with J's row set read behind the first product when `jr`
+  auto llt = [&](const A4Vec& r, bool jr) {
+    a4_ldt(CT, R, c);
+    const A4Vec y = a4_lmul(CL, r);
+    if (jr) a4_ldr(CR, R, c);
+    return a4_ltmul(CL, CT, y);
+  };
   // forward step k < N - 1: rhs, g, h = Linv' Linv g (stored), the next coupling J_k h
   auto fwd = [&](int k) {
     const double t1 = __dmul_rn(rv, __dsub_rn(z1, __dmul_rn(ri, y1)));
     const double init = lo12 ? __dmul_rn(ibk, tk) : 0.0;
-    A4Vec r = a4_jtmul(C, t1, A4Vec{init, 0.0, 0.0});
+    A4Vec r = a4_jtmul(CJ, t1, A4Vec{init, 0.0, 0.0});
     r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
     r.h16 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.x), hv1.x), r.h16);
     r.h17 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.y), hv1.y), r.h17);
     const double rc = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));  // k = 0: hc = 0
     r.lo = lo12 ? rc : r.lo;
-    const A4Vec h = a4_ltmul(C, a4_lmul(C, r));
-    a4_st(h.lo, rH, so(true, oT + 18 * k + c));
-    a4_st(c == 0 ? h.h16 : h.h17, rH, so(lo2, oT + 18 * k + c16));
-    hc.lo = a4_jmul(C, c, h);
+    const A4Vec h = llt(r, true);
+    a5_st(h.lo, rA, so(true, hT + 8u * (18 * k + c)));
+    a5_st(c == 0 ? h.h16 + 0.0 : h.h17 + 0.0, rA, so(lo2, hT + 8u * (18 * k + c16)));
+    hc.lo = a4_jmul(CR, c, h);
     tk = t1;
     ibk = ib1;
   };
@@ -1006,15 +1085,15 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
     r.lo = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));
     r.lo = lo12 ? r.lo : 0.0;
-    hc = a4_ltmul(C, a4_lmul(C, r));  // the backward sweep starts from xt_{N-1} = h_{N-1}
-    a4_st(hc.lo, rH, so(lo12, oT + 18 * k + c));
+    hc = llt(r, false);  // the backward sweep starts from xt_{N-1} = h_{N-1}
+    a5_st(hc.lo, rA, so(lo12, hT + 8u * (18 * k + c)));
   };
   // backward step k < N - 1: xt_k, then block k+1's rows and x_{k+1}
   auto bwd = [&](int k) {
     const double u = __dmul_rn(__dmul_rn(rv, ib1), hc.lo);
-    const A4Vec s2 = a4_ltmul(C, a4_lmul(C, a4_jtmul(C, u, A4Vec{0.0, 0.0, 0.0})));
+    const A4Vec s2 = llt(a4_jtmul(CJ, u, A4Vec{0.0, 0.0, 0.0}), true);
     const A4Vec xt{__dsub_rn(v0, s2.lo), __dsub_rn(hv0.x, s2.h16), __dsub_rn(hv0.y, s2.h17)};
-    const double zt = __dadd_rn(a4_jmul(C, c, xt), __dmul_rn(ib1, hc.lo));
+    const double zt = __dadd_rn(a4_jmul(CR, c, xt), __dmul_rn(ib1, hc.lo));
     const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z1));
     double zn = __dadd_rn(zr, __dmul_rn(ri, y1));
     zn = fmin(fmax(zn, l1), l1);
@@ -1023,11 +1102,11 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, hv1.x));
     const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, hv1.y));
     const bool last1 = k + 1 == N - 1;  // x_{k+1} has no u-part
-    const int ob = om + 12 * (k + 1) + c;
-    a4_st(zn, rZ, so(lo12, ob));
-    a4_st(yn, rY, so(lo12, ob));
-    a4_st(xn, rX, so(!last1 || lo12, oT + 18 * (k + 1) + c));
-    a4_st(c == 0 ? xn16 : xn17, rX, so(!last1 && lo2, oT + 18 * (k + 1) + c16));
+    const unsigned ob = 8u * (12 * (k + 1) + c);
+    a5_st(zn, rA, so(lo12, zM + ob));
+    a5_st(yn, rA, so(lo12, yM + ob));
+    a5_st(xn, rA, so(!last1 || lo12, xT + 8u * (18 * (k + 1) + c)));
+    a5_st(c == 0 ? xn16 + 0.0 : xn17 + 0.0, rA, so(!last1 && lo2, xT + 8u * (18 * (k + 1) + c16)));
     if (k == 0) {
       nx1 = xn;
       nx1h = make_double2(xn16, xn17);
@@ -1036,44 +1115,48 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     }
     hc = xt;
   };
+  // step s of an iteration (ring slot `slot`): forward k = s (< N - 1), the last forward step
+  // (s = N - 1), the backward sweep's start (s = N: xt_{N-1} = h_{N-1}, already in hc), backward
+  // k = 2N - 1 - s
+  int slot = 0;
   int it;
   for (it = 1; it <= a.A.max_iter; ++it) {
-    int s = 0;
-    for (int k = 0; k < N - 1; ++k, ++s) {
-      begin(s);
-      if (it > 1 && k == 0) {
-        v0 = nx0; hv0 = nx0h; z1 = nz1; y1 = ny1;
+    for (int s = 0; s < 2 * N; ++s) {
+      begin(s, slot);
+      if (s < N - 1) {
+        if (it > 1 && s == 0) {
+          v0 = nx0; hv0 = nx0h; z1 = nz1; y1 = ny1;
+        }
+        if (it > 1 && s == 1) {
+          v0 = nx1; hv0 = nx1h;
+        }
+        fwd(s);
+      } else if (s == N - 1) {
+        if (it > 1 && N == 2) v0 = nx1;  // (N = 2: the last forward step is stage 1)
+        fwd_last();
+      } else if (s > N) {
+        bwd(2 * N - 1 - s);
       }
-      if (it > 1 && k == 1) {
-        v0 = nx1; hv0 = nx1h;
-      }
-      fwd(k);
-    }
-    begin(s++);
-    if (it > 1 && N == 2) v0 = nx1;  // (N = 2: the last forward step is stage 1)
-    fwd_last();
-    begin(s++);  // backward k = N - 1: xt_{N-1} = h_{N-1} (in hc), nothing else
-    for (int k = N - 2; k >= 0; --k, ++s) {
-      begin(s);
-      bwd(k);
+      slot = slot == 2 ? 0 : slot + 1;
     }
     // block 0's rows (z~ = I xt_0) and x_0
     {
-      const double z0 = a4_ld(rZ, om + cc), y0 = a4_ld(rY, om + cc), l0 = a4_ld(rL, om + cc), i0 = a4_ld(rI, om + cc);
-      const double x0 = a4_ld(rX, oT + c);
-      const double2 x0h = a4_ld2(rX, oT + 16);
+      const double z0 = a5_ld(rA, zM + 8 * cc), y0 = a5_ld(rA, yM + 8 * cc), l0 = a5_ld(rA, lM + 8 * cc);
+      const double i0 = a5_ld(rA, iM + 8 * cc);
+      const double x0 = a5_ld(rA, xT + 8 * c);
+      const double x016 = a5_ld(rA, xT + 8 * 16), x017 = a5_ld(rA, xT + 8 * 17);
       const double zt = __dmul_rn(i0, hc.lo);
       const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z0));
       double zn = __dadd_rn(zr, __dmul_rn(ri, y0));
       zn = fmin(fmax(zn, l0), l0);
       const double yn = __dadd_rn(y0, __dmul_rn(rv, __dsub_rn(zr, zn)));
       const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, x0));
-      const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, x0h.x));
-      const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, x0h.y));
-      a4_st(zn, rZ, so(lo12, om + c));
-      a4_st(yn, rY, so(lo12, om + c));
-      a4_st(xn, rX, so(true, oT + c));
-      a4_st(c == 0 ? xn16 : xn17, rX, so(lo2, oT + c16));
+      const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, x016));
+      const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, x017));
+      a5_st(zn, rA, so(lo12, zM + 8u * c));
+      a5_st(yn, rA, so(lo12, yM + 8u * c));
+      a5_st(xn, rA, so(true, xT + 8u * c));
+      a5_st(c == 0 ? xn16 + 0.0 : xn17 + 0.0, rA, so(lo2, xT + 8u * c16));
       nx0 = xn;
       nx0h = make_double2(xn16, xn17);
       tk = __dmul_rn(rv, __dsub_rn(zn, __dmul_rn(ri, yn)));
@@ -1083,10 +1166,11 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const bool chk = a.A.check && it % a.A.check == 0;
     const bool adapt = ADAPT && a.A.adapt_interval && it % a.A.adapt_interval == 0;
     if (chk || adapt) {
+      a5_drain();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       double rest = rho;
-      const long bq = bb + prow;
+      const long bq = bown < P.B ? bown : bb;
       const bool ok = adm_check<16>(a, N, T, m, c_cost, rho, a.sx + bq * T, a.sz + bq * m, a.sy + bq * m, a.qs + bq * T,
                                     a.ls + bq * m, a.D + bq * T, a.E + bq * m, a.R + bq * N * ADM_REC + REC_J,
                                     a.I + bq * m, a.Pq + bq * N * 36, a.Pd + bq * T, &rest, c);
@@ -1108,37 +1192,31 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
             ri = 1.0 / rv;
           }
           // re-factor the rows whose rho moved, one problem at a time on the whole wave (the
-          // image is the factor's scratch)
+          // ring is the factor's scratch)
           for (int q = 0; q < 4; ++q) {
             if (!((mv >> (16 * q)) & 0xffff)) continue;
             const long bq2 = bb + q;
             const double rq = __shfl(rho, 16 * q, 64);
-            double* scr = sImg;
+            double* scr = ring;
             adm_factor(a, N, rq, a.Pq + bq2 * N * 36, a.Pd + bq2 * T, a.I + bq2 * m, a.R + bq2 * N * ADM_REC, scr,
                        scr + 30 * I7M_ADMM_FSTRIDE + 388, scr + 30 * I7M_ADMM_FSTRIDE, scr + 18 * I7M_ADMM_FSTRIDE, l);
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          for (int e = l; e < 4 * A4_PS; e += 64) sImg[e] = 0.0;
-          tk = __dmul_rn(rv, __dsub_rn(a4_ld(rZ, om + cc), __dmul_rn(ri, a4_ld(rY, om + cc))));
+          tk = __dmul_rn(rv, __dsub_rn(a5_ld(rA, zM + 8 * cc), __dmul_rn(ri, a5_ld(rA, yM + 8 * cc))));
           reload = true;
         }
       }
       if (!__ballot(run)) break;
-      if (__ballot(fin)) {
-        // finished rows read a running row's lines from here on
-        pick_shadow();
-        oT = prow * T;
-        om = prow * m;
-        oR = prow * N * ADM_REC;
-        reload = true;
-      }
+      if (__ballot(fin)) offsets();  // finished rows read nothing from here on
       if (reload) {
-        issue(A0, 0);
-        issue(A1, 1);
+        slot = 0;
+        issue(0, 0);
+        issue(1, 1);
       }
     }
   }
+  a5_drain();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (c == 0 && act) {

@@ -286,6 +286,8 @@ AdmmArgs admm_layout(double* base, int* its, long Bm, long N, long b0) {
   a.R = p[12]; a.w = p[13]; a.cs = p[14];
   a.iters = its + b0 * I7M_MAX_SQP;
   a.status = its + (Bm + b0) * I7M_MAX_SQP;
+  a.abase = base;  // k_admm_iter reaches every array through one buffer resource over the allocation
+  a.abytes = (long)(cur - base) * 8;
   return a;
 }
 size_t admm_doubles(long Bm, long N) {
@@ -1089,6 +1091,10 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
          alloc((void**)&h->d_bhinv, Bm * (N - 1) * 36 * 8) && alloc((void**)&h->d_bdh, Bm * T * 8) &&
          alloc((void**)&h->d_bst, Bm * sizeof(IpmState)) && alloc((void**)&h->d_bact, Bm * sizeof(int));
   if (ok && cfg->qp_mode == I7M_QP_ADMM) {
+    // k_admm_iter addresses the allocation with 32-bit byte offsets below its 0x7ff00000 marker
+    if (admm_doubles((long)Bm, (long)N) * 8 >= 0x7ff00000ull)
+      return bail(fail(I7M_EINVAL, "ADMM mode: max_batch=" + std::to_string(cfg->max_batch) + " at N=" + std::to_string(N) +
+                                       " needs over 2 GiB of ADMM state; use a smaller max_batch per handle"));
     ok = alloc((void**)&h->d_admm, admm_doubles((long)Bm, (long)N) * 8) &&
          alloc((void**)&h->d_admm_it, 2 * Bm * I7M_MAX_SQP * sizeof(int));
     h->cfg.qp_mode = I7M_QP_ADMM;

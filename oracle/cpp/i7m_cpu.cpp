@@ -1136,13 +1136,25 @@ struct Solver {
     }
     return a0 + a1;
   }
+  // sum_{c < 16} cf[c] v[c] as the device's a4_rowsum: t[c] = fma(cf[c], v[c], cf[c-1] v[c-1]),
+  // then t[c] += t[c - d] for d = 2, 4, 8 (a pairwise tree), the result t[15]
+  static double adm_rowsum(const double* cf, const double* v) {
+    double p[16], t[16];
+    for (int c = 0; c < 16; ++c) p[c] = cf[c] * v[c];
+    for (int c = 1; c < 16; ++c) t[c] = std::fma(cf[c], v[c], p[c - 1]);
+    t[0] = p[0];
+    for (int d = 2; d < 16; d *= 2)
+      for (int c = 15; c >= d; --c) t[c] = t[c] + t[c - d];
+    return t[15];
+  }
   // Linv_k (lower) and Linv_k' (upper) times an 18-vector, in the device's order (rows / columns
-  // 0..15 by adm_dot16, then the u-part's terms; the zeros above the diagonal add nothing)
+  // 0..15 by adm_dot16, rows 16, 17 by adm_rowsum, then the u-part's terms; the zeros above the
+  // diagonal add nothing)
   void lmul(int k, const double* v, double* o) const {
     const double* Li = &aLinv[324 * k];
     for (int c = 0; c < 16; ++c) o[c] = adm_dot16(Li + 18 * c, v);
-    o[16] = std::fma(Li[18 * 16 + 16], v[16], adm_dot16(Li + 18 * 16, v));
-    o[17] = std::fma(Li[18 * 17 + 17], v[17], std::fma(Li[18 * 17 + 16], v[16], adm_dot16(Li + 18 * 17, v)));
+    o[16] = std::fma(Li[18 * 16 + 16], v[16], adm_rowsum(Li + 18 * 16, v));
+    o[17] = std::fma(Li[18 * 17 + 17], v[17], std::fma(Li[18 * 17 + 16], v[16], adm_rowsum(Li + 18 * 17, v)));
   }
   void ltmul(int k, const double* v, double* o) const {
     const double* Li = &aLinv[324 * k];
