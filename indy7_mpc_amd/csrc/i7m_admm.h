@@ -726,51 +726,47 @@ struct A4Vec {
   double lo, h16, h17;
 };
 // acc += (lane n of the row's v) * coef: v_fmac_f64_dpp with the broadcast fused (DP DPP takes only
-// row_newbcast).  Four fma's per statement into four accumulators; the statement opens with the
-// two wait states a DPP read of a VGPR a VALU just wrote needs (the compiler pads no asm).
-// BM: the lanes written (bank b = lanes 4b..4b+3 of every row); the masked lanes keep their sums
-template <int n, int BM = 0xf>
-__device__ __forceinline__ void a4_fmac4(double& a0, double& a1, double& a2, double& a3, double v, double c0, double c1,
-                                         double c2, double c3) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:%9 row_mask:0xf bank_mask:%13\n\t"
-      "v_fmac_f64_dpp %1, %4, %6 row_newbcast:%10 row_mask:0xf bank_mask:%13\n\t"
-      "v_fmac_f64_dpp %2, %4, %7 row_newbcast:%11 row_mask:0xf bank_mask:%13\n\t"
-      "v_fmac_f64_dpp %3, %4, %8 row_newbcast:%12 row_mask:0xf bank_mask:%13"
-      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
-      : "v"(v), "v"(c0), "v"(c1), "v"(c2), "v"(c3), "i"(n), "i"(n + 1), "i"(n + 2), "i"(n + 3), "i"(BM));
-}
-template <int n>
-__device__ __forceinline__ void a4_fmac2(double& a0, double& a1, double v, double c0, double c1) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%6 row_mask:0xf bank_mask:0xf"
-      : "+v"(a0), "+v"(a1)
-      : "v"(v), "v"(c0), "v"(c1), "i"(n), "i"(n + 1));
-}
+// row_newbcast); the asm opens with the two wait states a DPP read of a VGPR a VALU just wrote
+// needs (the compiler pads no asm).  BM: the lanes written (bank b = lanes 4b..4b+3 of every row);
+// masked lanes keep their sums.
 // sum_{l < 16} coef[l] * v_l as four interleaved chains (l mod 4), combined (a0 + a1) + (a2 + a3):
 // the device's and the port's order (oracle/cpp/i7m_cpu.cpp adm_dot16).  TRI 1: lane c takes
 // terms l <= c only (a lower-triangular row: the terms of a group of four past lane c's bank are
-// masked, those inside it read the row's zero padding); TRI 2: terms l >= c only (a column).
+// masked, those inside it read the row's zero padding); TRI 2: terms l >= c only (a column).  One
+// asm statement: the compiler can put nothing between the fma's, so one pair of wait states (for
+// a DPP read of v just written) serves all sixteen.
 template <int TRI = 0>
 __device__ __forceinline__ double a4_dot16(double v, const double* cf) {
   constexpr int M0 = TRI == 1 ? 0xf : TRI == 2 ? 0x1 : 0xf, M1 = TRI == 1 ? 0xe : TRI == 2 ? 0x3 : 0xf;
   constexpr int M2 = TRI == 1 ? 0xc : TRI == 2 ? 0x7 : 0xf, M3 = TRI == 1 ? 0x8 : 0xf;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  a4_fmac4<0, M0>(a0, a1, a2, a3, v, cf[0], cf[1], cf[2], cf[3]);
-  a4_fmac4<4, M1>(a0, a1, a2, a3, v, cf[4], cf[5], cf[6], cf[7]);
-  a4_fmac4<8, M2>(a0, a1, a2, a3, v, cf[8], cf[9], cf[10], cf[11]);
-  a4_fmac4<12, M3>(a0, a1, a2, a3, v, cf[12], cf[13], cf[14], cf[15]);
+#define A4_F(acc, op, n, m) "v_fmac_f64_dpp " acc ", %4, " op " row_newbcast:" #n " row_mask:0xf bank_mask:" m "\n\t"
+  asm volatile(
+      "s_nop 1\n\t"
+      A4_F("%0", "%5", 0, "%21") A4_F("%1", "%6", 1, "%21") A4_F("%2", "%7", 2, "%21") A4_F("%3", "%8", 3, "%21")
+      A4_F("%0", "%9", 4, "%22") A4_F("%1", "%10", 5, "%22") A4_F("%2", "%11", 6, "%22") A4_F("%3", "%12", 7, "%22")
+      A4_F("%0", "%13", 8, "%23") A4_F("%1", "%14", 9, "%23") A4_F("%2", "%15", 10, "%23") A4_F("%3", "%16", 11, "%23")
+      A4_F("%0", "%17", 12, "%24") A4_F("%1", "%18", 13, "%24") A4_F("%2", "%19", 14, "%24") A4_F("%3", "%20", 15, "%24")
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+      : "v"(v), "v"(cf[0]), "v"(cf[1]), "v"(cf[2]), "v"(cf[3]), "v"(cf[4]), "v"(cf[5]), "v"(cf[6]), "v"(cf[7]),
+        "v"(cf[8]), "v"(cf[9]), "v"(cf[10]), "v"(cf[11]), "v"(cf[12]), "v"(cf[13]), "v"(cf[14]), "v"(cf[15]),
+        "i"(M0), "i"(M1), "i"(M2), "i"(M3));
+#undef A4_F
   return __dadd_rn(__dadd_rn(a0, a1), __dadd_rn(a2, a3));
 }
 // sum_{r = 6..11} coef[r - 6] * u_r as two chains (r even / odd), combined
 __device__ __forceinline__ double a4_dot6(double u, const double* cf) {
   double a0 = 0.0, a1 = 0.0;
-  a4_fmac2<6>(a0, a1, u, cf[0], cf[1]);
-  a4_fmac2<8>(a0, a1, u, cf[2], cf[3]);
-  a4_fmac2<10>(a0, a1, u, cf[4], cf[5]);
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f64_dpp %0, %2, %3 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %4 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %6 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %0, %2, %7 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %1, %2, %8 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+      : "+v"(a0), "+v"(a1)
+      : "v"(u), "v"(cf[0]), "v"(cf[1]), "v"(cf[2]), "v"(cf[3]), "v"(cf[4]), "v"(cf[5]));
   return __dadd_rn(a0, a1);
 }
 // sum over the row's 16 lanes of cf_c v_c (a pairwise tree: lane 15 gathers lanes 14, 12-13, 8-11,
@@ -886,8 +882,11 @@ __device__ __forceinline__ void a5_st(double v, __amdgpu_buffer_rsrc_t r, unsign
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(a4u2, v), r, off, 0, 0);
 }
 // one step's DMA: 10 record wave-instructions (per-lane offsets ro[t], the stage in soffset) and 3
-// vector ones (per-lane offsets vo[u]), to the slot at LDS byte address `lds` (M0 = the
-// wave-instruction's 1 KB, saved and restored around)
+// vector ones (per-lane offsets vo[u]), to the slot at LDS byte address `lds`.  The instruction
+// offset moves the LDS destination as well as the source (tools/probes/lds_dma_offset_probe), so
+// M0 (saved and restored around) steps by 4 KB every four wave-instructions and the per-lane
+// offsets carry -1 KB (t mod 4) (a5_dma_off).
+__device__ __forceinline__ unsigned a5_dma_off(int t) { return 1024u * (unsigned)(t & 3); }
 __device__ __forceinline__ void a5_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, const unsigned (&ro)[A5_RI], unsigned so,
                                        const unsigned (&vo)[A5_VI]) {
   unsigned keep;
@@ -895,23 +894,26 @@ __device__ __forceinline__ void a5_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, c
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %3, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %4, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %5, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %6, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %7, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %8, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %9, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %10, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %11, %15, %16 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %12, %15, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %13, %15, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %15, %16 offen lds\n\t"
+      "buffer_load_dwordx4 %3, %15, %16 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %4, %15, %16 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %5, %15, %16 offen offset:3072 lds\n\t"
+      "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %15, %16 offen lds\n\t"
+      "buffer_load_dwordx4 %7, %15, %16 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %8, %15, %16 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %9, %15, %16 offen offset:3072 lds\n\t"
+      "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %10, %15, %16 offen lds\n\t"
+      "buffer_load_dwordx4 %11, %15, %16 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %12, %15, 0 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %13, %15, 0 offen offset:3072 lds\n\t"
+      "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
       "buffer_load_dwordx4 %14, %15, 0 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "s"(lds), "v"(ro[0]), "v"(ro[1]), "v"(ro[2]), "v"(ro[3]), "v"(ro[4]), "v"(ro[5]), "v"(ro[6]), "v"(ro[7]),
-        "v"(ro[8]), "v"(ro[9]), "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(r), "s"(so)
+      : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(ro[0]), "v"(ro[1]), "v"(ro[2]), "v"(ro[3]), "v"(ro[4]), "v"(ro[5]), "v"(ro[6]), "v"(ro[7]),
+        "v"(ro[8]), "v"(ro[9]), "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "s"(r), "s"(__builtin_amdgcn_readfirstlane(so))
       : "memory");
 }
 // the step's slot has landed: at most 13 vector-memory operations in flight (the next step's DMA,
@@ -952,7 +954,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   // DMA source offsets of this lane's pieces (rows that do not run read nothing: out of range).
   // Records: piece g = 64 t + l of the four problems' 632; vectors: piece g = 64 u + l of their
   // 168, problem g / 42 piece j = g % 42: [0, 9) v0, [9, 18) v1, [18, 42) z, y, l, I (6 each).
-  unsigned ro[A5_RI], vF[A5_VI], vB[A5_VI];
+  unsigned ro[A5_RI], vF[A5_VI], vB[A5_VI], vD[A5_VI], vZ[A5_VI], vo[A5_VI];
   int vcls[A5_VI];
   auto offsets = [&]() {
     const unsigned long long rm = __ballot(run);
@@ -960,7 +962,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     for (int t = 0; t < A5_RI; ++t) {
       const int g = 64 * t + l, q = g / A5_RP, j = g - A5_RP * q;
       const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
-      ro[t] = ok ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * j : A5_OOB;
+      ro[t] = (ok ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * j : A5_OOB) - a5_dma_off(t);
     }
 #pragma unroll
     for (int u = 0; u < A5_VI; ++u) {
@@ -976,38 +978,54 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       } else {
         const int jj = j - 18, w = jj / 6;
         f = (w == 0 ? oZ + 0u : w == 1 ? oY + 0u : w == 2 ? oL + 0u : oI + 0u) + rM + 16u * (jj - 6 * w);
-        bk = f; cl = 2;
+        bk = f; cl = w == 0 ? 3 : 2;
       }
-      vF[u] = ok ? f : A5_OOB;
-      vB[u] = ok ? bk : A5_OOB;
+      const unsigned o = a5_dma_off(A5_RI + u);
+      vF[u] = (ok ? f : A5_OOB) - o;
+      vB[u] = (ok ? bk : A5_OOB) - o;
+      vD[u] = ok ? (cl < 2 ? 144u : 96u) : 0u;  // bytes per stage
+      vZ[u] = ok && cl == 3 ? oL - oZ : 0u;     // z's pieces from l's lines
       vcls[u] = cl;
     }
   };
   offsets();
-  // issue step s's DMA (s < 2N) into ring slot `slot`: its stage record; forward: x_k, q_k;
-  // backward: h_k, x_{k+1}; both: block k+1's z, y, l, I (the last stage's missing block reads
-  // block N-1's, unused)
-  auto issue = [&](int s, int slot) {
+  // step s's vector offsets from scratch (s < 2N): forward: x_k, q_k; backward: h_k, x_{k+1};
+  // both: block k+1's z, y, l, I (the last stage's missing block reads block N-1's, unused).
+  // (zl: the step is past the first iteration, where z = l: every block's projection onto its
+  // equality rows, fmin(fmax(., l), l), is l itself, so z's pieces come from l's lines)
+  auto vfull = [&](int s, bool zl) {
     const bool fwd = s < N;
     const int k = fwd ? s : 2 * N - 1 - s;
     const int k1 = k + 1 < N ? k + 1 : N - 1;
     const int kb = fwd ? k : k1;
+#pragma unroll
+    for (int u = 0; u < A5_VI; ++u) {
+      const unsigned st = vcls[u] == 0 ? 144u * k : (vcls[u] == 1 ? 144u * kb : 96u * k1);
+      vo[u] = (fwd ? vF[u] + 0u : vB[u] + 0u) + (zl ? vZ[u] + st : st);
+    }
+  };
+  // issue step s's DMA into ring slot `slot`: the vector offsets advance by one stage (forward
+  // steps 1..N-2 and backward steps N+2.. are the previous step's one stage on) or are recomputed
+  auto issue = [&](int s, int slot, bool zl) {
+    const bool fwd = s < N;
+    const int k = fwd ? s : 2 * N - 1 - s;
+    if (s == 0 || s == N - 1 || s == N || s == N + 1) {
+      vfull(s, zl);
+    } else {
+#pragma unroll
+      for (int u = 0; u < A5_VI; ++u) vo[u] = fwd ? vo[u] + vD[u] : vo[u] - vD[u];
+    }
 #ifdef I7M_DIAG
     // I7M_ABLATE 21: every step reads stage 0's record (L2-resident: the sweep without its stream)
     const unsigned so = 8u * (unsigned)(a.ablate == 21 ? 0 : k * ADM_REC);
 #else
     const unsigned so = 8u * (unsigned)(k * ADM_REC);
 #endif
-    unsigned vo[A5_VI];
-#pragma unroll
-    for (int u = 0; u < A5_VI; ++u) {
-      const unsigned st = vcls[u] == 0 ? 144u * k : (vcls[u] == 1 ? 144u * kb : 96u * k1);
-      vo[u] = (fwd ? vF[u] + 0u : vB[u] + 0u) + st;
-    }
     a5_dma(rA, ring_lds + 16u * A5_SLOT * slot, ro, so, vo);
   };
-  issue(0, 0);
-  issue(1, 1);
+  issue(0, 0, false);
+  issue(1, 1, false);
+  int it = 1;
   // carried between steps
   A4Vec hc{0.0, 0.0, 0.0};  // forward: J_{k-1} h_{k-1} (lanes 0..11) / backward: xt_{k+1}
   double tk = __dmul_rn(rv, __dsub_rn(a5_ld(rA, zM + 8 * cc), __dmul_rn(ri, a5_ld(rA, yM + 8 * cc))));  // block k's t
@@ -1026,21 +1044,17 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   A4CR CR;
   const double* R = nullptr;
   // one step's start: wait for its slot, issue step s + 2's DMA into the slot step s - 1 used, read
-  // the step's vectors and the first two coefficient sets
-  auto begin = [&](int s, int slot) {
+  // the step's vectors (rows ci of v0, cb of v1: the last stage's 12 rows clamped) and the first
+  // two coefficient sets
+  auto begin = [&](int s, int slot, int ci, int cb) {
     a5_wait();
     int sn = s + 2, sl = slot + 2;
     if (sn >= 2 * N) sn -= 2 * N;
     if (sl >= 3) sl -= 3;
-    issue(sn, sl);
+    issue(sn, sl, it > 1 || sn < s);
     const double* S = ring + 2 * A5_SLOT * slot;
     R = S + ADM_REC * p;
     const double* V = S + A5_VD + 2 * A5_VP * p;  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
-    const bool last = s == N - 1 || s == N;       // stage N-1: 12 rows
-    // (prvalue selects: a conditional of two captured lvalues becomes a select of their addresses
-    // and a memory load, which waits for every DMA in flight)
-    const int ci = last ? (c < 12 ? c : 11) : c + 0;
-    const int cb = s == N - 1 || s == N || s == N + 1 ? (c < 12 ? c : 11) : c + 0;
     v0 = V[ci];
     v1 = V[18 + cb];
     hv0 = make_double2(V[16], V[17]);
@@ -1103,7 +1117,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, hv1.y));
     const bool last1 = k + 1 == N - 1;  // x_{k+1} has no u-part
     const unsigned ob = 8u * (12 * (k + 1) + c);
-    a5_st(zn, rA, so(lo12, zM + ob));
+    a5_st(zn, rA, so(lo12 && it == 1, zM + ob));  // (l from the second iteration on: already stored)
     a5_st(yn, rA, so(lo12, yM + ob));
     a5_st(xn, rA, so(!last1 || lo12, xT + 8u * (18 * (k + 1) + c)));
     a5_st(c == 0 ? xn16 + 0.0 : xn17 + 0.0, rA, so(!last1 && lo2, xT + 8u * (18 * (k + 1) + c16)));
@@ -1115,29 +1129,33 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     }
     hc = xt;
   };
-  // step s of an iteration (ring slot `slot`): forward k = s (< N - 1), the last forward step
-  // (s = N - 1), the backward sweep's start (s = N: xt_{N-1} = h_{N-1}, already in hc), backward
-  // k = 2N - 1 - s
+  // an iteration's 2N steps (ring slot `slot` = the step count mod 3): forward k = s < N - 1, the
+  // last forward step (s = N - 1), the backward sweep's start (s = N: xt_{N-1} = h_{N-1}, already in
+  // hc), backward k = 2N - 1 - s; each segment a loop of its own (no per-step dispatch)
   int slot = 0;
-  int it;
-  for (it = 1; it <= a.A.max_iter; ++it) {
-    for (int s = 0; s < 2 * N; ++s) {
-      begin(s, slot);
-      if (s < N - 1) {
-        if (it > 1 && s == 0) {
-          v0 = nx0; hv0 = nx0h; z1 = nz1; y1 = ny1;
-        }
-        if (it > 1 && s == 1) {
-          v0 = nx1; hv0 = nx1h;
-        }
-        fwd(s);
-      } else if (s == N - 1) {
-        if (it > 1 && N == 2) v0 = nx1;  // (N = 2: the last forward step is stage 1)
-        fwd_last();
-      } else if (s > N) {
-        bwd(2 * N - 1 - s);
+  auto next = [&]() { slot = slot == 2 ? 0 : slot + 1; };
+  for (; it <= a.A.max_iter; ++it) {
+    for (int s = 0; s < N - 1; ++s) {
+      begin(s, slot, c, c);
+      if (it > 1 && s == 0) {
+        v0 = nx0; hv0 = nx0h; z1 = nz1; y1 = ny1;
       }
-      slot = slot == 2 ? 0 : slot + 1;
+      if (it > 1 && s == 1) {
+        v0 = nx1; hv0 = nx1h;
+      }
+      fwd(s);
+      next();
+    }
+    begin(N - 1, slot, cc, cc);
+    if (it > 1 && N == 2) v0 = nx1;  // (N = 2: the last forward step is stage 1)
+    fwd_last();
+    next();
+    begin(N, slot, cc, cc);
+    next();
+    for (int s = N + 1; s < 2 * N; ++s) {
+      begin(s, slot, c, s == N + 1 ? cc : c + 0);
+      bwd(2 * N - 1 - s);
+      next();
     }
     // block 0's rows (z~ = I xt_0) and x_0
     {
@@ -1153,7 +1171,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, x0));
       const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, x016));
       const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, x017));
-      a5_st(zn, rA, so(lo12, zM + 8u * c));
+      a5_st(zn, rA, so(lo12 && it == 1, zM + 8u * c));
       a5_st(yn, rA, so(lo12, yM + 8u * c));
       a5_st(xn, rA, so(true, xT + 8u * c));
       a5_st(c == 0 ? xn16 + 0.0 : xn17 + 0.0, rA, so(lo2, xT + 8u * c16));
@@ -1208,11 +1226,14 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
         }
       }
       if (!__ballot(run)) break;
-      if (__ballot(fin)) offsets();  // finished rows read nothing from here on
+      if (__ballot(fin)) {  // finished rows read nothing from here on
+        offsets();
+        vfull(1, true);  // (the running vector offsets: the last issued step's)
+      }
       if (reload) {
         slot = 0;
-        issue(0, 0);
-        issue(1, 1);
+        issue(0, 0, true);
+        issue(1, 1, true);
       }
     }
   }
