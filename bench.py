@@ -266,11 +266,12 @@ def config4(model, stream, local: int, steps: int, warmup: int, B: int = 4096, N
 
 
 def admm_bytes_per_iter(N: int):
-    """HBM bytes one OSQP iteration of k_admm_iter streams per problem (i7m_admm.h): the forward and the
-    backward sweep each read every stage's record (ADM_REC = 292 doubles: packed Linv_k 171, compact
-    scaled J_k 120, one pad; the coupling block is never stored), plus the per-knot vectors (x, q, z,
-    y, w, the scaling rows: ~120 doubles per knot)."""
-    return 8 * (2 * 292 * N + 120 * N)
+    """HBM bytes one OSQP iteration of k_admm_iter moves per problem (i7m_admm.h), per stage: the
+    forward and the backward sweep each DMA the stage record (ADM_REC = 300 doubles: Linv_k with
+    rows padded to even widths 180, compact scaled J_k 120; the coupling block is never stored) and
+    the step's vectors (x or h, q or x: 18 each; y, l, I: 12 each; z reads l's lines after the first
+    iteration), and the sweeps store h, y and x (18 + 12 + 18)."""
+    return 8 * N * (2 * 300 + 2 * 72 + 48)
 
 
 def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 32, native=None,

@@ -84,23 +84,32 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_ITER_WPE
 #define I7M_ADMM_ITER_WPE 2  // ... and k_admm_iter without adaptive rho (at 3: 78 spilled VGPRs, 30% slower)
 #endif
-constexpr int ADM_LP = 196, ADM_JC = 120;
+constexpr int ADM_LP = 180, ADM_JC = 120;
 // One record per stage, N per problem (problem b's at R + b N ADM_REC): [Linv_k | compact J_k]
-// = 316 doubles (158 pieces of 16 B).  Linv_k's rows 0-15 are stored lower-triangular with each
-// row padded with zeros to a multiple of four entries (widths 4, 8, 12, 16: 160 doubles), rows 16
-// and 17 in full (36): every lane's row and column reads in k_admm_iter are then a base plus a
-// constant, and the entries past a padded row are never read (the DPP fma's bank masks skip
-// them).  k_admm_iter streams the record twice per OSQP iteration (forward and backward sweep);
-// the coupling C_k = M_{k+1,k} Linv_k' of the factor is never stored: the sweeps apply it as
-// re I_{k+1} J_k and the triangular pair.
-constexpr int ADM_REC = 316, REC_J = ADM_LP;
+// = 300 doubles (150 pieces of 16 B).  Linv_k's rows 0-15 are stored lower-triangular, each padded
+// to an even width (a zero after the diagonal of the even rows: 144 doubles), rows 16 and 17 in full
+// (36); J_k as its q rows' two diagonals (J[i][i], J[i][6 + i]) and its v rows (6 x 18).
+// k_admm_iter streams the record twice per OSQP iteration (forward and backward sweep) into LDS,
+// where its DMA lays Linv's rows 0-15 out at widths of four (A5_LREC: the extra pieces read as
+// zeros), so every lane's row and column reads are a base plus a constant and the entries past a
+// row's width are never read (the DPP fma's bank masks skip them).  The coupling
+// C_k = M_{k+1,k} Linv_k' of the factor is never stored: the sweeps apply it as re I_{k+1} J_k and
+// the triangular pair.
+constexpr int ADM_REC = 300, REC_J = ADM_LP;
 // entry (i, j) of Linv_k in the record, and the stored width of row i
-__device__ __forceinline__ int adm_lw(int i) { return i < 16 ? 4 * (i / 4 + 1) : 18; }
+__device__ __forceinline__ int adm_lw(int i) { return i < 16 ? 2 * ((i + 2) / 2) : 18; }
 __device__ __forceinline__ int adm_lrow(int i) {
+  const int h = i >> 1;  // rows 2h, 2h+1 have width 2h + 2
+  return i < 16 ? 2 * h * (h + 1) + (i & 1) * (2 * h + 2) : 144 + 18 * (i - 16);
+}
+__device__ __forceinline__ int adm_lrec(int i, int j) { return adm_lrow(i) + j; }
+// the LDS image of a record (k_admm_iter): rows 0-15 at widths 4, 8, 12, 16 (160 doubles), rows 16
+// and 17 (36), J (120)
+constexpr int A5_LREC = 316, A5_LJ = 196;
+__device__ __forceinline__ int a5_lrow(int i) {
   const int g = i >> 2;
   return i < 16 ? 8 * g * (g + 1) + 4 * (g + 1) * (i - 4 * g) : 160 + 18 * (i - 16);
 }
-__device__ __forceinline__ int adm_lrec(int i, int j) { return adm_lrow(i) + j; }
 // dense 12 x 18 J_k into LDS from its compact form
 __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
   for (int e = l; e < 216; e += 64) {
@@ -693,7 +702,7 @@ constexpr int A5_RI = 10;                      // record DMA wave-instructions p
 constexpr int A5_VI = 3;                       // vector DMA wave-instructions per step (192 >= 4 x 42 pieces)
 constexpr int A5_SLOT = 64 * (A5_RI + A5_VI);  // 16-B pieces per ring slot (13 KB)
 constexpr int A5_VP = 42;                      // vector pieces per problem and step
-constexpr int A5_RP = ADM_REC / 2;             // record pieces per problem and stage (158)
+constexpr int A5_RP = A5_LREC / 2;             // LDS record pieces per problem and stage (158)
 constexpr int A5_VD = 2 * 64 * A5_RI;          // the slot's vector part (doubles)
 constexpr unsigned A5_OOB = 0x7ff00000u;       // a byte offset past every allocation (< 2 GiB enforced by the host)
 template <int n>
@@ -804,7 +813,7 @@ struct A4CR {
   double Jr[18], Jq0, Jq1;  // J row c (v rows 6..11; clamped outside them), J[q][q], J[q][6 + q] (q = c < 6 ? c : 0)
 };
 __device__ __forceinline__ void a4_ldj(A4CJ& C, const double* R, int c) {
-  const double* J = R + REC_J;  // [J[i][i] (6) | J[i][6 + i] (6) | v rows 6 x 18]
+  const double* J = R + A5_LJ;  // [J[i][i] (6) | J[i][6 + i] (6) | v rows 6 x 18]
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     C.Jt[r] = J[12 + 18 * r + c];
@@ -829,7 +838,7 @@ __device__ __forceinline__ void a4_ldt(A4CT& C, const double* R, int c) {
   for (int l = 0; l < 16; ++l) C.Lt[l] = R[rs[l] + c];
 }
 __device__ __forceinline__ void a4_ldr(A4CR& C, const double* R, int c) {
-  const double* J = R + REC_J;
+  const double* J = R + A5_LJ;
   const int rr = c < 6 ? 0 : (c < 12 ? c - 6 : 5);
 #pragma unroll
   for (int l = 0; l < 18; ++l) C.Jr[l] = J[12 + 18 * rr + l];
@@ -962,7 +971,19 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     for (int t = 0; t < A5_RI; ++t) {
       const int g = 64 * t + l, q = g / A5_RP, j = g - A5_RP * q;
       const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
-      ro[t] = (ok ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * j : A5_OOB) - a5_dma_off(t);
+      // LDS piece j of the record -> its piece in HBM (rows 0-15 from width 4 to the stored even
+      // width: the pieces past it read as zeros)
+      int hp;
+      if (j < 80) {
+        int r = 0;
+#pragma unroll
+        for (int i = 1; i < 16; ++i) r = 2 * j >= a5_lrow(i) ? i : r;
+        const int cp = 2 * j - a5_lrow(r);
+        hp = cp < adm_lw(r) ? (adm_lrow(r) + cp) / 2 : -1;
+      } else {
+        hp = j - 8;  // rows 16, 17 and J: HBM piece 72 + (j - 80) / 90 + (j - 98)
+      }
+      ro[t] = (ok && hp >= 0 ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * hp : A5_OOB) - a5_dma_off(t);
     }
 #pragma unroll
     for (int u = 0; u < A5_VI; ++u) {
@@ -1028,12 +1049,13 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   int it = 1;
   // carried between steps
   A4Vec hc{0.0, 0.0, 0.0};  // forward: J_{k-1} h_{k-1} (lanes 0..11) / backward: xt_{k+1}
-  double tk = __dmul_rn(rv, __dsub_rn(a5_ld(rA, zM + 8 * cc), __dmul_rn(ri, a5_ld(rA, yM + 8 * cc))));  // block k's t
-  double ibk = a5_ld(rA, iM + 8 * cc);
-  // the state the backward sweep hands to the next forward sweep's first two steps (their DMA was
-  // issued before the backward sweep wrote them)
-  double nx0 = 0.0, nx1 = 0.0, nz1 = 0.0, ny1 = 0.0;
-  double2 nx0h = make_double2(0.0, 0.0), nx1h = make_double2(0.0, 0.0);
+  // block 0's rows and x_0 (only the epilogue updates them) and the state the backward sweep hands
+  // to the next forward sweep's first two steps (their DMA was issued before the sweep wrote them)
+  double b0z = a5_ld(rA, zM + 8 * cc), b0y = a5_ld(rA, yM + 8 * cc), b0l = a5_ld(rA, lM + 8 * cc), b0i = a5_ld(rA, iM + 8 * cc);
+  double nx0 = a5_ld(rA, xT + 8 * c), nx1 = 0.0, nz1 = 0.0, ny1 = 0.0;
+  double2 nx0h = make_double2(a5_ld(rA, xT + 8 * 16), a5_ld(rA, xT + 8 * 17)), nx1h = make_double2(0.0, 0.0);
+  double tk = __dmul_rn(rv, __dsub_rn(b0z, __dmul_rn(ri, b0y)));  // block k's t
+  double ibk = b0i;
   int done_it = 0;
   bool solved = false;
   double v0, v1, z1, y1, l1, ib1;
@@ -1053,7 +1075,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     if (sl >= 3) sl -= 3;
     issue(sn, sl, it > 1 || sn < s);
     const double* S = ring + 2 * A5_SLOT * slot;
-    R = S + ADM_REC * p;
+    R = S + A5_LREC * p;
     const double* V = S + A5_VD + 2 * A5_VP * p;  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
     v0 = V[ci];
     v1 = V[18 + cb];
@@ -1064,7 +1086,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     l1 = V[60 + cc];
     ib1 = V[72 + cc];
     a4_ldj(CJ, R, c);
-    a4_ldl(CL, R, R + adm_lrow(c), c);
+    a4_ldl(CL, R, R + a5_lrow(c), c);
   };
   // store offsets: masked (past the range) for rows that do not run
   auto so = [&](bool ok, unsigned off) { return run && ok ? off + 0u : A5_OOB + 0u; };
@@ -1159,10 +1181,8 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     }
     // block 0's rows (z~ = I xt_0) and x_0
     {
-      const double z0 = a5_ld(rA, zM + 8 * cc), y0 = a5_ld(rA, yM + 8 * cc), l0 = a5_ld(rA, lM + 8 * cc);
-      const double i0 = a5_ld(rA, iM + 8 * cc);
-      const double x0 = a5_ld(rA, xT + 8 * c);
-      const double x016 = a5_ld(rA, xT + 8 * 16), x017 = a5_ld(rA, xT + 8 * 17);
+      // (block 0 is the epilogue's alone: its state rides in registers across iterations)
+      const double z0 = b0z, y0 = b0y, l0 = b0l, i0 = b0i, x0 = nx0, x016 = nx0h.x, x017 = nx0h.y;
       const double zt = __dmul_rn(i0, hc.lo);
       const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z0));
       double zn = __dadd_rn(zr, __dmul_rn(ri, y0));
@@ -1177,6 +1197,8 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       a5_st(c == 0 ? xn16 + 0.0 : xn17 + 0.0, rA, so(lo2, xT + 8u * c16));
       nx0 = xn;
       nx0h = make_double2(xn16, xn17);
+      b0z = zn;
+      b0y = yn;
       tk = __dmul_rn(rv, __dsub_rn(zn, __dmul_rn(ri, yn)));
       ibk = i0;
       hc = A4Vec{0.0, 0.0, 0.0};
@@ -1221,7 +1243,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          tk = __dmul_rn(rv, __dsub_rn(a5_ld(rA, zM + 8 * cc), __dmul_rn(ri, a5_ld(rA, yM + 8 * cc))));
+          tk = __dmul_rn(rv, __dsub_rn(b0z, __dmul_rn(ri, b0y)));
           reload = true;
         }
       }
