@@ -76,7 +76,7 @@ struct AdmmArgs {
 #define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
 #ifndef I7M_ADMM_SCALE_WPE
-#define I7M_ADMM_SCALE_WPE 3  // (127 VGPRs, 12 KB LDS: 3 waves per SIMD; 2.11 -> 2.08 ms prep)
+#define I7M_ADMM_SCALE_WPE 2  // (N <= 32: the linearisation magnitudes stay in registers for all ten passes)
 #endif
 #ifndef I7M_ADMM_FACTOR_WPE
 #define I7M_ADMM_FACTOR_WPE 2
@@ -309,10 +309,10 @@ template <int CT>
 __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int T, int m, const double* LIN,
                                             const double* CO, const double* QD, const double* X, double* qold,
                                             double* Pq, double* Pd, double* Jb, double* Ib, double* qs, double* ls,
-                                            double* D, double* E, double* sD, double* sE, double* sDt, int l) {
+                                            double* D, double* E, double* sD, double* sE, double* sDt, double* sRM, int l) {
   constexpr int RT = 2 * CT / 3;
   const double dt = a.P.dt;
-  double qv[CT], etv[RT];
+  double qv[CT], etv[RT], dtv[CT <= 9 ? CT : 1];  // (a lane's q entries and its columns' / rows' pass factors)
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int e = l + 64 * t;
@@ -337,12 +337,61 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
     const double pd = j < 12 ? w[7] : w[8];
     return j < 6 ? mq : fabs(pd) * (dj * dj) * c;
   };
+  // N <= 32 (CT <= 9): the linearisation's 108 v-row entries of stage k live in the registers of
+  // lanes 2k (rows 6-8 of block k + 1) and 2k + 1 (rows 9-11) for all passes, read once: each pass
+  // forms their scaled magnitudes (E_i |a_ij|) D_j once, for both the row maxima (sRM) and, with the
+  // partner lane's three rows, the column maxima (sDt); max is exact, so every norm is the port's.
+  constexpr bool REG = CT <= 9;
+  const int ks = l >> 1, hs = l & 1;
+  const bool sv = REG && ks < N - 1;
+  double av[REG ? 3 : 1][REG ? 18 : 1];
+  if constexpr (REG) {
+    const double* L = LIN + LIN_STRIDE * (sv ? ks : 0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int j = 0; j < 18; ++j) {
+        const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
+        av[r][j] = sv ? fabs(L[jb + 6 * (3 * hs + r)]) : 0.0;
+      }
+  }
   for (int pass = 0; pass < a.A.scaling; ++pass) {
     // every pass recomputes its indices (hoisted out of the pass loop they would take ~300 VGPRs)
     const double* Lp = LIN;
     const double* Cp = CO;
     int lp = l;
     asm volatile("" : "+v"(lp));
+    if constexpr (REG) {
+      double cm[18];
+#pragma unroll
+      for (int j = 0; j < 18; ++j) cm[j] = 0.0;
+      const int kq = sv ? ks : 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double er = sE[12 * (kq + 1) + 6 + 3 * hs + r];
+        double rm = 0.0;
+#pragma unroll
+        for (int j = 0; j < 18; ++j) {
+          const double pv = er * av[r][j] * sD[18 * kq + j];
+          rm = fmax(rm, pv);
+          cm[j] = fmax(cm[j], pv);
+        }
+        if (sv) sRM[12 * (kq + 1) + 6 + 3 * hs + r] = rm;
+      }
+      // the partner lane's rows (DPP quad_perm [1,0,3,2]), then lane h stores columns 9h..9h+8
+#pragma unroll
+      for (int j = 0; j < 18; ++j) {
+        const long long u = __double_as_longlong(cm[j]);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)u, 0xB1, 0xf, 0xf, true);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0xB1, 0xf, 0xf, true);
+        cm[j] = fmax(cm[j], __longlong_as_double(((long long)hi << 32) | (unsigned int)lo));
+      }
+      if (sv) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) sDt[18 * kq + 9 * hs + j] = hs ? cm[9 + j] : cm[j];
+      }
+      wave_sync_fence();
+    }
 #pragma unroll 3
     for (int t = 0; t < CT; ++t) {
       const int e = min(lp + 64 * t, T - 1), k = e / 18, j = e - 18 * k;
@@ -358,10 +407,16 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
       const double eid = Eb[j < 6 ? j : (j < 12 ? j - 6 : 0)] * (j < 6 ? 1.0 : dt) * dj;
       double mj = j < 12 ? eid : 0.0;
+      if constexpr (REG) {
+        mj = fmax(mj, sDt[e]);  // (the stage owners' max over the six v rows)
+      } else {
 #pragma unroll
-      for (int r = 0; r < 6; ++r) mj = fmax(mj, Eb[6 + r] * fabs(L[jb + 6 * r]) * dj);
+        for (int r = 0; r < 6; ++r) mj = fmax(mj, Eb[6 + r] * fabs(L[jb + 6 * r]) * dj);
+      }
       if (k < N - 1) mx = fmax(mx, mj);
-      sDt[lp + 64 * t] = 1.0 / sqrt(adm_limit(mx));
+      // (a lane's own pass factors: registers at N <= 32, LDS at the wide variant's register count)
+      if constexpr (REG) dtv[t] = 1.0 / sqrt(adm_limit(mx));
+      else sDt[lp + 64 * t] = 1.0 / sqrt(adm_limit(mx));
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -370,16 +425,21 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       double mx = er * sD[18 * blk + i];
       // row i of J_{blk-1} (block 0's rows are -I on x_0 alone)
       const int kk = blk > 0 ? blk - 1 : 0;
-      const double* L = Lp + LIN_STRIDE * kk;
       const double* Db = sD + 18 * kk;
-      // rows 0-5: the identity and dt entries; rows 6-11: 18 linearisation entries
+      // rows 0-5: the identity and dt entries; rows 6-11: 18 linearisation entries (at N <= 32
+      // their max from the stage owners)
       const int i6 = i < 6 ? i : i - 6;
       const double mi = fmax(er * 1.0 * Db[i6], er * dt * Db[6 + i6]);
       double ml = 0.0;
+      if constexpr (REG) {
+        ml = sRM[r];
+      } else {
+        const double* L = Lp + LIN_STRIDE * kk;
 #pragma unroll
-      for (int j = 0; j < 18; ++j) {
-        const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
-        ml = fmax(ml, er * fabs(L[jb + 6 * i6]) * Db[j]);
+        for (int j = 0; j < 18; ++j) {
+          const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
+          ml = fmax(ml, er * fabs(L[jb + 6 * i6]) * Db[j]);
+        }
       }
       const double mj = i < 6 ? mi : ml;
       if (blk > 0) mx = fmax(mx, mj);
@@ -389,7 +449,9 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
       const int e = lp + 64 * t;
-      const double dtt = sDt[e];
+      double dtt;
+      if constexpr (CT <= 9) dtt = dtv[t];
+      else dtt = sDt[e];
       if (e < T) sD[e] = sD[e] * dtt;
       qv[t] = dtt * qv[t];
     }
@@ -645,9 +707,8 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   if (b >= P.B || (a.active && !a.active[b])) return;
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
   constexpr bool FAC = (PH & 8) != 0;
-  // (k_admm_scale: sB holds the column scale factors of a Ruiz pass)
   __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1];
-  __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1];
+  __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1], sRM[(PH & 1) ? 64 * (2 * CT / 3) : 1];
   double* sL = sB;
   double* sJ = sB + 540;
   const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -665,7 +726,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   double* D = a.D + (long)b * T;
   double* E = a.E + (long)b * m;
   if constexpr (PH & 1) {
-    const double c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, l);
+    const double c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, sRM, l);
     if (l == 0) a.cs[b] = c;
   }
   if constexpr (PH & 8) {
