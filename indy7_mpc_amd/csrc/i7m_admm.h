@@ -708,7 +708,8 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   const int l = threadIdx.x, N = P.N, T = P.T, m = 12 * N;
   constexpr bool FAC = (PH & 8) != 0;
   __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1];
-  __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1], sRM[(PH & 1) ? 64 * (2 * CT / 3) : 1];
+  __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1], sRM[(PH & 1) ? 64 * (2 * CT / 3) : 1],
+      sCO[(PH & 1) ? (64 * CT / 18 + 1) * COST_STRIDE : 1];
   double* sL = sB;
   double* sJ = sB + 540;
   const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -726,7 +727,9 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   double* D = a.D + (long)b * T;
   double* E = a.E + (long)b * m;
   if constexpr (PH & 1) {
-    const double c = adm_scale<CT>(a, b, N, T, m, LIN, CO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, sRM, l);
+    // the cost blocks every pass reads, in LDS for the launch
+    for (int e = l; e < N * COST_STRIDE; e += 64) sCO[e] = CO[e];
+    const double c = adm_scale<CT>(a, b, N, T, m, LIN, sCO, QD, X, qold, Pq, Pd, Jb, Ib, qs, ls, D, E, sD, sE, sB, sRM, l);
     if (l == 0) a.cs[b] = c;
   }
   if constexpr (PH & 8) {

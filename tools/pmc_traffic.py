@@ -50,7 +50,7 @@ def main():
     f = per_kernel(a.fetch, "FETCH_SIZE")
     w = per_kernel(a.write, "WRITE_SIZE")
     grids = {"k_linearize": -(-a.batch * a.N // 10) * 64, "k_riccati": a.batch * 64, "k_linesearch": a.batch * 64,
-             "k_ipm_fused": a.batch * 64, "k_sqp_fused": a.batch * 64, "k_admm_iter": a.batch * 64,
+             "k_ipm_fused": a.batch * 64, "k_sqp_fused": a.batch * 64, "k_admm_iter": -(-a.batch // 4) * 64,
              "k_admm_scale": a.batch * 64, "k_admm_factor": a.batch * 64}
     try:
         d = json.load(open(a.out))
