@@ -110,6 +110,16 @@ __device__ __forceinline__ int a5_lrow(int i) {
   const int g = i >> 2;
   return i < 16 ? 8 * g * (g + 1) + 4 * (g + 1) * (i - 4 * g) : 160 + 18 * (i - 16);
 }
+// Buffer-resource access (k_admm_factor's and k_admm_iter's DMA and stores): a uniform base in
+// SGPRs, 32-bit per-lane byte offsets, the hardware's range check (an offset past the range reads
+// zeros and drops stores: A5_OOB masks lanes without branches)
+constexpr unsigned A5_OOB = 0x7ff00000u;  // a byte offset past every allocation (< 2 GiB enforced by the host)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t a4_rsrc(const void* base, long bytes) {
+  const unsigned long long u = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
 // dense 12 x 18 J_k into LDS from its compact form
 __device__ __forceinline__ void adm_stage_J(double* sJ, const double* Jc, int l) {
   for (int e = l; e < 216; e += 64) {
@@ -528,12 +538,48 @@ __device__ __forceinline__ double adm_readlane(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane((int)u, lane), hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// A stage's operands arrive one stage ahead by LDS DMA into `stg` (two buffers of 256 doubles:
+// compact J_k 120 | P_k's quadratic block 36 | its diagonal 18 | I_k 12 | I_{k+1} 12), so no stage
+// waits on a global load; the DMA (inline asm, the compiler does not see it) is waited for by a
+// counted s_waitcnt at the next stage's start.
+constexpr int AF_STG = 256;
 __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho, const double* Pq, const double* Pd, const double* Ib,
-                           double* Rb, double* sS, double* sJ, double* sL, double* sCp, int l0) {
+                           double* Rb, double* sS, double* sJ, double* sL, double* sCp, double* stg, int l0) {
   const double re = 1e3 * rho, sigma = a.A.sigma;
-  const int T = 18 * N - 6;
   constexpr int FS = I7M_ADMM_FSTRIDE;  // row stride of S and C_{k-1} in LDS
   double* sCol = sL + 324;  // (the sweeps' C slot, free while factoring)
+  const auto rA = a4_rsrc(a.abase, a.abytes);
+  auto boff = [&](const double* q) { return (unsigned)__builtin_amdgcn_readfirstlane((int)((const char*)q - (const char*)a.abase)); };
+  const unsigned oR = boff(Rb), oPq = boff(Pq), oPd = boff(Pd), oI = boff(Ib);
+  const unsigned stg_lds = (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)stg;
+  // stage k's pieces: lane l's piece g = l (+ 64): [0, 60) J, [60, 78) Pq, [78, 87) Pd, [87, 93) I_k,
+  // [93, 99) I_{k+1}, past 99 nothing
+  auto fetch = [&](int k) {
+    unsigned vo[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int g = 64 * u + l0;
+      unsigned o;
+      if (g < 60) o = oR + 8u * (unsigned)(ADM_REC * k + REC_J) + 16u * g;
+      else if (g < 78) o = oPq + 8u * (unsigned)(36 * k) + 16u * (g - 60);
+      else if (g < 87) o = oPd + 8u * (unsigned)(18 * k) + 16u * (g - 78);
+      else if (g < 99) o = oI + 8u * (unsigned)(12 * k) + 16u * (g - 87);
+      else o = A5_OOB;
+      vo[u] = o - 1024u * u;
+    }
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %4, 0 offen lds\n\t"
+        "buffer_load_dwordx4 %3, %4, 0 offen offset:1024 lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(__builtin_amdgcn_readfirstlane(stg_lds + 8u * AF_STG * (k & 1))), "v"(vo[0]), "v"(vo[1]), "s"(rA)
+        : "memory");
+  };
+  fetch(0);
   for (int k = 0; k < N; ++k) {
     const int nk = k < N - 1 ? 18 : 12;
     // every stage recomputes the lane's indices (hoisted out of the stage loop they would take
@@ -541,16 +587,23 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     int l = l0;
     asm volatile("" : "+v"(l));
     const int lr = l < 18 ? l : 17;  // lanes 18-63 shadow lane 17 (never read back)
-    if (k < N - 1) adm_stage_J(sJ, Rb + ADM_REC * k + REC_J, l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage k's operands have landed
+    if (k + 1 < N) fetch(k + 1);
+    const double* G = stg + AF_STG * (k & 1);
+    if (k < N - 1) adm_stage_J(sJ, G, l);
     wave_sync();
+    // S is symmetric to the bit (every term's products commute and sum in the same order), so the
+    // lanes form its lower triangle (171 entries) and mirror it
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
+    for (int t = 0; t < 3; ++t) {
       const int e = l + 64 * t;
-      if (e < 324) {
-        const int i = e / 18, j = e - 18 * i, ic = i < 12 ? i : 11, jc = j < 12 ? j : 11;
-        const double pq = Pq[36 * k + 6 * (i < 6 ? i : 0) + (j < 6 ? j : 0)];
-        const double pd = Pd[min(18 * k + i, T - 1)];
-        const double ib = Ib[12 * k + ic];
+      if (e < 171) {
+        int i = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+        i = (i + 1) * (i + 2) / 2 <= e ? i + 1 : (i * (i + 1) / 2 > e ? i - 1 : i);
+        const int j = e - i * (i + 1) / 2, ic = i < 12 ? i : 11, jc = j < 12 ? j : 11;
+        const double pq = G[120 + 6 * (i < 6 ? i : 0) + (j < 6 ? j : 0)];
+        const double pd = G[156 + i];  // (the last stage's rows past 12: overwritten below)
+        const double ib = G[174 + ic];
         const double dj = adm_dot2<12>(0.0, sJ + i, 18, sJ + j, 18);
         const double dc = adm_dot2<18>(0.0, sCp + FS * ic, 1, sCp + FS * jc, 1);
         double v = i < 6 && j < 6 ? pq : (i == j && i >= 6 ? pd : 0.0);
@@ -560,6 +613,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
         if (k > 0 && i < 12 && j < 12) v -= dc;
         if (i >= nk || j >= nk) v = i == j ? 1.0 : 0.0;
         sS[FS * i + j] = v;
+        sS[FS * j + i] = v;
       }
     }
     wave_sync();
@@ -613,12 +667,14 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
         if (e < 216) {
           const int i = e / 18, j = e - 18 * i;
           const double acc = adm_dot2<18>(0.0, sJ + 18 * i, 1, sL + 18 * j, 1);
-          const double cv = re * Ib[12 * (k + 1) + i] * acc;
+          const double cv = re * G[186 + i] * acc;
           sCp[FS * i + j] = cv;
         }
       }
     }
-    wave_sync_all();
+    // (LDS only: the stage's global stores are read by no later stage, and the kernel's end or the
+    // re-factoring caller's fence orders them; a global release here waited for them every stage)
+    wave_sync_fence();
   }
 }
 
@@ -709,7 +765,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
   constexpr bool FAC = (PH & 8) != 0;
   __shared__ double sB[(PH & 1) ? 64 * CT : 756], sS[FAC ? 18 * I7M_ADMM_FSTRIDE : 1], sCp[FAC ? 12 * I7M_ADMM_FSTRIDE : 1];
   __shared__ double sD[(PH & 1) ? 64 * CT : 1], sE[(PH & 1) ? 64 * (2 * CT / 3) : 1], sRM[(PH & 1) ? 64 * (2 * CT / 3) : 1],
-      sCO[(PH & 1) ? (64 * CT / 18 + 1) * COST_STRIDE : 1];
+      sCO[(PH & 1) ? (64 * CT / 18 + 1) * COST_STRIDE : 1], sStg[FAC ? 2 * AF_STG : 1];
   double* sL = sB;
   double* sJ = sB + 540;
   const double* LIN = a.lin + (long)b * (N - 1) * LIN_STRIDE;
@@ -736,7 +792,7 @@ __device__ __forceinline__ void admm_body(const AdmmArgs& a) {
 #if I7M_ADMM_FACTOR == 1
     adm_factor_lds(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
 #else
-    adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, l);
+    adm_factor(a, N, a.srho[b], Pq, Pd, Ib, Rb, sS, sJ, sL, sCp, sStg, l);
 #endif
   }
 }
@@ -768,7 +824,6 @@ constexpr int A5_SLOT = 64 * (A5_RI + A5_VI);  // 16-B pieces per ring slot (13 
 constexpr int A5_VP = 42;                      // vector pieces per problem and step
 constexpr int A5_RP = A5_LREC / 2;             // LDS record pieces per problem and stage (158)
 constexpr int A5_VD = 2 * 64 * A5_RI;          // the slot's vector part (doubles)
-constexpr unsigned A5_OOB = 0x7ff00000u;       // a byte offset past every allocation (< 2 GiB enforced by the host)
 template <int n>
 __device__ __forceinline__ double a4_bc(double v) {  // lane n of the 16-lane row, to every lane of it
   return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + n, 0xf, 0xf, false);
@@ -942,12 +997,6 @@ __device__ __forceinline__ double a4_jmul(const A4CR& C, int c, const A4Vec& v) 
 }
 
 typedef unsigned int a4u2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t a4_rsrc(const void* base, long bytes) {
-  const unsigned long long u = (unsigned long long)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
-  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
-}
 __device__ __forceinline__ double a5_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
@@ -1303,7 +1352,8 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
             const double rq = __shfl(rho, 16 * q, 64);
             double* scr = ring;
             adm_factor(a, N, rq, a.Pq + bq2 * N * 36, a.Pd + bq2 * T, a.I + bq2 * m, a.R + bq2 * N * ADM_REC, scr,
-                       scr + 30 * I7M_ADMM_FSTRIDE + 388, scr + 30 * I7M_ADMM_FSTRIDE, scr + 18 * I7M_ADMM_FSTRIDE, l);
+                       scr + 30 * I7M_ADMM_FSTRIDE + 388, scr + 30 * I7M_ADMM_FSTRIDE, scr + 18 * I7M_ADMM_FSTRIDE,
+                       scr + 2048, l);
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
