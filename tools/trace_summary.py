@@ -3,7 +3,8 @@
 
     python tools/trace_summary.py RUN_kernel_trace.csv [--batch B --N N] > profiles/rNN_kernel_trace_summary.json
 
-With --batch, only launches of that batch size count (grid B*64 for the per-problem kernels,
+With --batch, only launches of that batch size count (grid B*64 for the per-problem kernels, B/4*64
+for k_admm_iter,
 ceil(B*N/10)*64 for k_linearize): bench.py also runs B = 1 and host-to-host solves.
 """
 import collections
@@ -30,7 +31,9 @@ def main(path, batch=None, N=32):
         name = CANON.get(name, name)
         if batch is not None and name.startswith("k_"):
             grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
-            want = -(-batch * N // 10) * 64 if name == "k_linearize" else batch * 64
+            want = (-(-batch * N // 10) * 64 if name == "k_linearize"
+                    else -(-batch // 4) * 64 if name == "k_admm_iter"  # (four problems per wave)
+                    else batch * 64)
             if grid != want:
                 continue
         d[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
