@@ -180,6 +180,9 @@ int i7m_abi_version(void);                        /* == I7M_ABI_VERSION of the h
 int i7m_config_default(i7m_config* cfg);          /* fills everything but `model` */
 int i7m_device_count(int* n);
 
+/* In ADMM mode the handle's OSQP state (about 4 KB x N per problem) must stay under 2 GiB: the
+   iteration kernel addresses it with 32-bit offsets; a larger max_batch x N is refused with
+   I7M_EINVAL (shard the batch over handles instead). */
 int i7m_create(const i7m_config* cfg, i7m_handle** out);
 void i7m_destroy(i7m_handle* h);
 /* NULL -> the handle's own stream, a blocking stream (ordered with the legacy null stream) */
