@@ -248,3 +248,11 @@ def test_admm_iteration_record_is_reset_every_solve(lib, model):
         n = r2["qp_iters"][b]
         assert (it2[b, :n] > 0).all() and (it2[b, n:] == -1).all(), (b, n, it2[b])
         assert (st2[b, :n] >= 0).all() and (st2[b, n:] == -1).all(), (b, n, st2[b])
+
+
+def test_admm_state_over_2gib_is_refused(lib, model):
+    """k_admm_iter addresses the handle's ADMM state with 32-bit offsets: i7m_create refuses a
+    max_batch x N whose state would pass 2 GiB (before allocating anything), with a message."""
+    with pytest.raises(Exception, match="2 GiB"):
+        lib.Handle(model, N=64, max_batch=200000, qp_mode=lib.QP_ADMM)
+
