@@ -362,7 +362,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 #pragma unroll
       for (int j = 0; j < 18; ++j) {
         const int jb = j < 6 ? j : (j < 12 ? 30 + j : 60 + j);
-        av[r][j] = sv ? fabs(L[jb + 6 * (3 * hs + r)]) : 0.0;
+        av[r][j] = sv ? L[jb + 6 * (3 * hs + r)] : 0.0;  // (signed: the J output below uses it too)
       }
   }
   for (int pass = 0; pass < a.A.scaling; ++pass) {
@@ -382,7 +382,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
         double rm = 0.0;
 #pragma unroll
         for (int j = 0; j < 18; ++j) {
-          const double pv = er * av[r][j] * sD[18 * kq + j];
+          const double pv = er * fabs(av[r][j]) * sD[18 * kq + j];
           rm = fmax(rm, pv);
           cm[j] = fmax(cm[j], pv);
         }
@@ -495,14 +495,31 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
     const int k = x / 36, q = x - 36 * k, i = q / 6, j = q - 6 * i;
     Pq[x] = adm_pq(CO + COST_STRIDE * k, i, j) * (sD[18 * k + i] * sD[18 * k + j]) * c;
   }
+  if constexpr (REG) {
+    // J_k by its stage owners, from the registers (rows 6 + 3h .. 8 + 3h, and q rows 3h .. 3h + 2)
+    if (sv) {
+      double* Jk = Jb + ADM_REC * ks;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int i = 3 * hs + r;
+        const double ev = sE[12 * (ks + 1) + 6 + i];
+#pragma unroll
+        for (int j = 0; j < 18; ++j) Jk[12 + 18 * i + j] = ev * av[r][j] * sD[18 * ks + j];
+        const double eq = sE[12 * (ks + 1) + i];
+        Jk[i] = eq * 1.0 * sD[18 * ks + i];
+        Jk[6 + i] = eq * dt * sD[18 * ks + 6 + i];
+      }
+    }
+  } else {
 #pragma unroll 4
-  for (int x = l; x < 120 * (N - 1); x += 64) {
-    const int k = x / 120, e = x - 120 * k;
-    int i, j;
-    if (e < 6) { i = e; j = e; }
-    else if (e < 12) { i = e - 6; j = e; }
-    else { i = 6 + (e - 12) / 18; j = (e - 12) % 18; }
-    Jb[ADM_REC * k + e] = sE[12 * (k + 1) + i] * adm_jk(LIN + LIN_STRIDE * k, dt, i, j) * sD[18 * k + j];
+    for (int x = l; x < 120 * (N - 1); x += 64) {
+      const int k = x / 120, e = x - 120 * k;
+      int i, j;
+      if (e < 6) { i = e; j = e; }
+      else if (e < 12) { i = e - 6; j = e; }
+      else { i = 6 + (e - 12) / 18; j = (e - 12) % 18; }
+      Jb[ADM_REC * k + e] = sE[12 * (k + 1) + i] * adm_jk(LIN + LIN_STRIDE * k, dt, i, j) * sD[18 * k + j];
+    }
   }
   for (int r = l; r < m; r += 64) {
     const int k = r / 12, i = r - 12 * k;
