@@ -42,14 +42,16 @@ def _rel(a, b):
     return np.linalg.norm(a - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-300)
 
 
-@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43), (16, 512, 41), (64, 24, 48), (5, 16, 49)])
+@pytest.mark.parametrize("N,B,seed", [(16, 8, 41), (32, 64, 43), (16, 512, 41), (64, 24, 48), (5, 16, 49), (32, 13, 50),
+                                       (2, 6, 51)])
 def test_admm_solves_match_port(lib, model, N, B, seed):
     """Two consecutive solves (the second warm-started from the first's OSQP state) on the GPU and
     on the port: same OSQP iterations and steps, same XU and state.  (16, 512, 41) holds problems
     whose first line search finds no step (alpha = 0): src/osqp_sqp.py:81-82 re-solves the same QP,
     which OSQP's warm start makes a different iterate — the GPU re-solves too (k_linesearch mode 2).
-    N = 64 runs the scaling kernel's wide variant; N = 5 a short horizon (B not a multiple of the
-    kernels' problems per wave is covered by B = 24 at N = 64)."""
+    N = 64 runs the scaling kernel's wide variant; N = 5 a short horizon, N = 2 the shortest (every
+    sweep step a segment end); B = 13 and 6 leave rows of k_admm_iter's last wave (four problems per
+    wave) empty."""
     xcur, goals, XU = synthetic_batch(B, N, seed)
     h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
     st = cpu.AdmmState(B, N)
