@@ -637,10 +637,12 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     double r[18];
 #pragma unroll
     for (int j = 0; j < 18; ++j) r[j] = sS[FS * lr + j];
+    double myid = 1.0;  // 1 / L_ll of this lane's row (the inverse multiplies by it)
 #pragma unroll
     for (int p = 0; p < 18; ++p) {
       const double d = sqrt(adm_readlane(r[p], p));
       const double id = 1.0 / d;
+      myid = l == p ? id : myid;
       r[p] = l == p ? d : (l > p ? r[p] * id : r[p]);
       if (p < 17) {
         // column p of L to the wave through LDS (double-buffered: no wait for the last reads)
@@ -652,9 +654,11 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       }
     }
     wave_sync();  // every lane has read S before L overwrites it
+    static_assert(FS >= 19, "the row's spare column holds 1 / L_ii");
     if (l < 18) {
 #pragma unroll
       for (int j = 0; j < 18; ++j) sS[FS * l + j] = r[j];
+      sS[FS * l + 18] = myid;
     }
     wave_sync();
     double x[18];
@@ -666,7 +670,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       double acc = 0.0;
 #pragma unroll
       for (int q = 0; q < i; ++q) acc += sS[o + q] * x[q];
-      x[i] = ((i == lr ? 1.0 : 0.0) - acc) / sS[o + i];
+      x[i] = ((i == lr ? 1.0 : 0.0) - acc) * sS[o + 18];  // (the port's order: by 1 / L_ii)
     }
     if (l < 18) {
 #pragma unroll

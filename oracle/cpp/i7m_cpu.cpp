@@ -1088,11 +1088,14 @@ struct Solver {
             for (int j = 0; j < 18; ++j) acc += Cp[a][j] * Cp[b][j];
             S[a][b] -= acc;
           }
-      // right-looking Cholesky (the GPU's lane-parallel order)
+      // right-looking Cholesky (the GPU's lane-parallel order); the pivots' reciprocals kept for
+      // the inverse (the device's: a product by 1 / L_ii, not a quotient)
+      double idv[18];
       for (int p = 0; p < nk; ++p) {
         const double d = std::sqrt(S[p][p]);
         S[p][p] = d;
         const double id = 1.0 / d;
+        idv[p] = id;
         for (int i = p + 1; i < nk; ++i) S[i][p] = S[i][p] * id;
         for (int i = p + 1; i < nk; ++i)
           for (int j = p + 1; j <= i; ++j) S[i][j] = S[i][j] - S[i][p] * S[j][p];
@@ -1100,11 +1103,11 @@ struct Solver {
       double* Li = &aLinv[324 * k];
       for (int i = 0; i < 324; ++i) Li[i] = 0.0;
       for (int j = 0; j < nk; ++j) {
-        Li[18 * j + j] = 1.0 / S[j][j];
+        Li[18 * j + j] = idv[j];
         for (int i = j + 1; i < nk; ++i) {
           double acc = 0.0;
           for (int l = j; l < i; ++l) acc += S[i][l] * Li[18 * l + j];
-          Li[18 * i + j] = -acc / S[i][i];
+          Li[18 * i + j] = -acc * idv[i];
         }
       }
       if (k < N - 1) {
