@@ -234,7 +234,10 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
                           double* rho_est, int l) {
   double pr = 0.0, zn = 0.0, an = 0.0, pri = 0.0, pn = 0.0;
   double dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0, dua = 0.0, dn = 0.0, xPx = 0.0, qx = 0.0, sc = 0.0;
-  // rows: block 0 = I x_0, block k+1 = J_k z_k + I x_{k+1}
+  // rows: block 0 = I x_0, block k+1 = J_k z_k + I x_{k+1}.  J's structural zeros are skipped
+  // (a q row has two entries: J[i][i], J[i][6 + i]); the other terms keep their order, so the
+  // sums are the full loop's (0 * x adds nothing).  Two rows / columns per lane in flight.
+#pragma unroll 2
   for (int r = l; r < m; r += W) {
     const int k = r / 12, i = r - 12 * k;
     double ax;
@@ -244,7 +247,14 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
       const double* G = Jb + ADM_REC * (k - 1);
       const double* xk = x + 18 * (k - 1);
       double acc = 0.0;
-      for (int j = 0; j < 18; ++j) acc += adm_jc(G, i, j) * xk[j];
+      if (i < 6) {
+        acc += G[i] * xk[i];
+        acc += G[6 + i] * xk[6 + i];
+      } else {
+        const double* Gr = G + 12 + 18 * (i - 6);
+#pragma unroll
+        for (int j = 0; j < 18; ++j) acc += Gr[j] * xk[j];
+      }
       ax = acc + Ib[r] * x[18 * k + i];
     }
     const double ei = 1.0 / E[r];
@@ -255,6 +265,7 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     pn = fmax(pn, fmax(fabs(z[r]), fabs(ax)));
     sc += ls[r] * fmax(y[r], 0.0) + ls[r] * fmin(y[r], 0.0);
   }
+#pragma unroll 2
   for (int e = l; e < T; e += W) {
     const int k = e / 18, j = e - 18 * k;
     double px;
@@ -268,7 +279,12 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
     double aty = j < 12 ? Ib[12 * k + j] * y[12 * k + j] : 0.0;
     if (k < N - 1) {
       const double* G = Jb + ADM_REC * k;
-      for (int i = 0; i < 12; ++i) aty += adm_jc(G, i, j) * y[12 * (k + 1) + i];
+      const double* yk = y + 12 * (k + 1);
+      // column j's q-row entry (row j or j - 6) comes before the v rows, as in the full loop
+      if (j < 6) aty += G[j] * yk[j];
+      else if (j < 12) aty += G[j] * yk[j - 6];
+#pragma unroll
+      for (int i = 6; i < 12; ++i) aty += G[12 + 18 * (i - 6) + j] * yk[i];
     }
     const double di = 1.0 / D[e];
     dr = fmax(dr, fabs(di * ((qs[e] + px) + aty)));
