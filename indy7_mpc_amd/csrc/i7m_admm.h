@@ -224,6 +224,14 @@ __device__ __forceinline__ void adm_sweep_sync() {
 #endif
 }
 
+// All of a row's (column's) loads issued before its first product: one memory round trip, not
+// the default schedule's one per eight loads.
+#define ADM_CHK_LOADS_FIRST()                          \
+  do {                                                 \
+    __builtin_amdgcn_sched_group_barrier(0x020, 24, 0); \
+    __builtin_amdgcn_sched_group_barrier(0x002, 96, 0); \
+  } while (0)
+
 // OSQP's check_termination on the unscaled residuals (+ the duality gap) and, for adapt_rho,
 // the scaled residual ratios; x, z, y scaled.  Returns solved; rho_est gets the estimate.  W lanes
 // share one problem (lane l of W): 64 (one problem per wave) or 16 (k_admm_iter: a 16-lane row).
@@ -235,66 +243,76 @@ __device__ bool adm_check(const AdmmArgs& a, int N, int T, int m, double c, doub
   double pr = 0.0, zn = 0.0, an = 0.0, pri = 0.0, pn = 0.0;
   double dr = 0.0, qn = 0.0, atn = 0.0, pxn = 0.0, dua = 0.0, dn = 0.0, xPx = 0.0, qx = 0.0, sc = 0.0;
   // rows: block 0 = I x_0, block k+1 = J_k z_k + I x_{k+1}.  J's structural zeros are skipped
-  // (a q row has two entries: J[i][i], J[i][6 + i]); the other terms keep their order, so the
-  // sums are the full loop's (0 * x adds nothing).  Two rows / columns per lane in flight.
-#pragma unroll 2
+  // (a q row has two entries: J[i][i], J[i][6 + i]; a column at most one q-row entry); the other
+  // terms keep their order, so the sums are the full loops' (0 * x adds nothing).
   for (int r = l; r < m; r += W) {
     const int k = r / 12, i = r - 12 * k;
-    double ax;
-    if (k == 0) {
-      ax = Ib[r] * x[i];
-    } else {
-      const double* G = Jb + ADM_REC * (k - 1);
-      const double* xk = x + 18 * (k - 1);
-      double acc = 0.0;
-      if (i < 6) {
-        acc += G[i] * xk[i];
-        acc += G[6 + i] * xk[6 + i];
-      } else {
-        const double* Gr = G + 12 + 18 * (i - 6);
+    // Every operand is loaded up front, from clamped (always valid) addresses, and the branches
+    // are selects: one memory round trip per row (the lanes of a wave take both paths anyway).
+    const int kk = k > 0 ? k - 1 : 0, iq = i < 6 ? i : 0, iv = i < 6 ? 0 : i - 6;
+    const double* G = Jb + ADM_REC * kk;
+    const double* xk = x + 18 * kk;
+    const double* Gr = G + 12 + 18 * iv;
+    const double ib = Ib[r], xr = x[18 * k + i], er = E[r], zr = z[r], yr = y[r], lr = ls[r];
+    const double ga = G[iq], gb = G[6 + iq], xa = xk[iq], xb = xk[6 + iq];
+    double gv[18], xv[18];
 #pragma unroll
-        for (int j = 0; j < 18; ++j) acc += Gr[j] * xk[j];
-      }
-      ax = acc + Ib[r] * x[18 * k + i];
+    for (int j = 0; j < 18; ++j) {
+      gv[j] = Gr[j];
+      xv[j] = xk[j];
     }
-    const double ei = 1.0 / E[r];
-    pr = fmax(pr, fabs(ei * (ax - z[r])));
-    zn = fmax(zn, fabs(ei * z[r]));
+    ADM_CHK_LOADS_FIRST();
+    double aq = 0.0, av = 0.0;  // a q row's two entries, a v row's 18
+    aq += ga * xa;
+    aq += gb * xb;
+#pragma unroll
+    for (int j = 0; j < 18; ++j) av += gv[j] * xv[j];
+    const double acc = i < 6 ? aq : av;
+    const double ax = k == 0 ? ib * xr : acc + ib * xr;
+    const double ei = 1.0 / er;
+    pr = fmax(pr, fabs(ei * (ax - zr)));
+    zn = fmax(zn, fabs(ei * zr));
     an = fmax(an, fabs(ei * ax));
-    pri = fmax(pri, fabs(ax - z[r]));
-    pn = fmax(pn, fmax(fabs(z[r]), fabs(ax)));
-    sc += ls[r] * fmax(y[r], 0.0) + ls[r] * fmin(y[r], 0.0);
+    pri = fmax(pri, fabs(ax - zr));
+    pn = fmax(pn, fmax(fabs(zr), fabs(ax)));
+    sc += lr * fmax(yr, 0.0) + lr * fmin(yr, 0.0);
   }
-#pragma unroll 2
   for (int e = l; e < T; e += W) {
     const int k = e / 18, j = e - 18 * k;
-    double px;
-    if (j < 6) {
-      double acc = 0.0;
-      for (int jj = 0; jj < 6; ++jj) acc += Pq[36 * k + 6 * j + jj] * x[18 * k + jj];
-      px = acc;
-    } else {
-      px = Pd[e] * x[e];
-    }
-    double aty = j < 12 ? Ib[12 * k + j] * y[12 * k + j] : 0.0;
-    if (k < N - 1) {
-      const double* G = Jb + ADM_REC * k;
-      const double* yk = y + 12 * (k + 1);
-      // column j's q-row entry (row j or j - 6) comes before the v rows, as in the full loop
-      if (j < 6) aty += G[j] * yk[j];
-      else if (j < 12) aty += G[j] * yk[j - 6];
+    // as the rows: clamped addresses, selects for the branches
+    const int jq = j < 12 ? j : 0, jc = j < 6 ? j : 0, kc = k < N - 1 ? k : 0;
+    const int jy = j < 6 ? j : (j < 12 ? j - 6 : 0);  // column j's q-row entry: row j or j - 6
+    const double* G = Jb + ADM_REC * kc;
+    const double* yk = y + 12 * (k < N - 1 ? k + 1 : 0);
+    const double xe = x[e], de = D[e], qe = qs[e], pde = Pd[e], ibj = Ib[12 * k + jq], yj = y[12 * k + jq];
+    const double gq = G[jq], yq = yk[jy];
+    double pq[6], xq[6], gv[6], yv[6];
 #pragma unroll
-      for (int i = 6; i < 12; ++i) aty += G[12 + 18 * (i - 6) + j] * yk[i];
+    for (int t = 0; t < 6; ++t) {
+      pq[t] = Pq[36 * k + 6 * jc + t];
+      xq[t] = x[18 * k + t];
+      gv[t] = G[12 + 18 * t + j];
+      yv[t] = yk[6 + t];
     }
-    const double di = 1.0 / D[e];
-    dr = fmax(dr, fabs(di * ((qs[e] + px) + aty)));
-    qn = fmax(qn, fabs(di * qs[e]));
+    ADM_CHK_LOADS_FIRST();
+    double pa = 0.0;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) pa += pq[t] * xq[t];
+    const double px = j < 6 ? pa : pde * xe;
+    const double at0 = j < 12 ? ibj * yj : 0.0;
+    double at1 = j < 12 ? at0 + gq * yq : at0;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) at1 += gv[t] * yv[t];
+    const double aty = k < N - 1 ? at1 : at0;
+    const double di = 1.0 / de;
+    dr = fmax(dr, fabs(di * ((qe + px) + aty)));
+    qn = fmax(qn, fabs(di * qe));
     atn = fmax(atn, fabs(di * aty));
     pxn = fmax(pxn, fabs(di * px));
-    dua = fmax(dua, fabs(qs[e] + px + aty));
-    dn = fmax(dn, fmax(fabs(qs[e]), fmax(fabs(aty), fabs(px))));
-    xPx += x[e] * px;
-    qx += qs[e] * x[e];
+    dua = fmax(dua, fabs(qe + px + aty));
+    dn = fmax(dn, fmax(fabs(qe), fmax(fabs(aty), fabs(px))));
+    xPx += xe * px;
+    qx += qe * xe;
   }
   pr = adm_max<W>(pr); zn = adm_max<W>(zn); an = adm_max<W>(an); pri = adm_max<W>(pri); pn = adm_max<W>(pn);
   dr = adm_max<W>(dr); qn = adm_max<W>(qn); atn = adm_max<W>(atn); pxn = adm_max<W>(pxn);
