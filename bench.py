@@ -321,7 +321,8 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
     h.close()
     el = float(np.mean(times))
     used = it[it >= 0]
-    res = {"workload": f"config3 ADMM: B={B}, N={N}, OSQP's iteration per QP (I7M_QP_ADMM), cold OSQP state each step",
+    res = {"workload": f"config3 ADMM: B={B}, N={N}, OSQP's iteration per QP (I7M_QP_ADMM), cold OSQP state each step"
+                       + (", two staggered ranges (i7m_handle::admm_stagger)" if B >= 4096 else ""),
            "value": B / el, "unit": "solves/s", "ms_per_step": 1e3 * el, "steps": steps,
            "osqp_iters_per_qp": {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())},
            "qp_iters_mean": float(st["qp_iters"].mean()), "finite": bool(np.isfinite(out).all()),
@@ -342,6 +343,11 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
                            "factor_stream": {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,
                                              "achieved_GBs": stream_gbs, "frac": stream_gbs / HBM_PEAK_GBS,
                                              "note": "the blocks every OSQP iteration re-reads (bench.admm_bytes_per_iter)"}}
+        # the same bytes over the whole step (every kernel of both SQP iterations): with the
+        # staggered ranges a launch shares the GPU with the other range's kernels, so its own
+        # duration understates what the stream achieves
+        step_gbs = ipl * (cnt // steps) * admm_bytes_per_iter(N) / el / 1e9
+        res["roofline"]["factor_stream"].update({"step_achieved_GBs": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS})
     # the reference's use: a closed loop whose every QP warm-starts from the instance's last one
     res["closed_loop"] = mpc_closed_loop(model, stream, local, B, N, steps=10, qp_mode=_lib.QP_ADMM)
     if native is not None:

@@ -140,6 +140,18 @@ struct i7m_handle {
   int h2h_chunks = 0;
   int admm_chunk = 0;  // I7M_ADMM_CHUNK: k_admm launched over this many problems at a time (0: all)
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
+  // ADMM mode, i7m_solve_device with B >= admm_stagger_min_b: the batch as admm_ranges ranges on
+  // streams of their own, each started once the one before has passed a mark (1: its first QP's
+  // scaling and factor; 2: its first QP), so one range's latency-bound phases (the factor, the
+  // OSQP iterations after the first termination check) overlap another's stream-bound ones
+  // (DESIGN.md §4.7).  0: one range.  I7M_ADMM_STAGGER, I7M_ADMM_RANGES, I7M_ADMM_STAGGER_MIN_B.
+  int admm_stagger = 1;
+  int admm_ranges = 2;
+  int admm_stagger_min_b = 4096;  // measured: B = 4096 +17 %; B = 2048 / 1024 -8 / -11 % (two ranges)
+  static constexpr int kMaxRanges = 4;
+  hipStream_t rs[kMaxRanges] = {};  // ranges 2.. (0 and 1 run on cs[0], cs[1]); created on first use
+  hipEvent_t ev_rmark[kMaxRanges] = {}, ev_rdone[kMaxRanges] = {};
+  hipEvent_t mark_ev = nullptr;  // set: solve_qp records it at the mark, once, and clears it
   hipStream_t cs[2] = {nullptr, nullptr};
   hipStream_t cs2 = nullptr;  // h2h_pipe >= 2: the second solve stream (created on first use)
   hipEvent_t ev_order = nullptr, ev_done[2] = {nullptr, nullptr};
@@ -539,6 +551,10 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
         hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
       });
       if (rc2) return rc2;
+      if (h->mark_ev && h->admm_stagger == 1) {
+        HIPCHK(hipEventRecord(h->mark_ev, s));
+        h->mark_ev = nullptr;
+      }
       rc2 = timed(h, s, I7M_K_ADMM, [&](hipEvent_t ea, hipEvent_t eb) {
         // four problems per wave: the launch covers [lo, lo + n) (a.b0 = lo), rows past it idle
         SolveParams P4 = a.P;
@@ -552,6 +568,10 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
           hipExtLaunchKernelGGL(k_admm_iter<false>, g, dim3(64), 0, s, ea, eb, 0, a4);
       });
       if (rc2) return rc2;
+    }
+    if (h->mark_ev && h->admm_stagger == 2) {
+      HIPCHK(hipEventRecord(h->mark_ev, s));
+      h->mark_ev = nullptr;
     }
     return I7M_OK;
   }
@@ -1053,6 +1073,10 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_H2H_TAPER")) h->h2h_taper = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_ADMM_CHUNK")) h->admm_chunk = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
+  if (const char* e = std::getenv("I7M_ADMM_STAGGER")) h->admm_stagger = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("I7M_ADMM_STAGGER_MIN_B")) h->admm_stagger_min_b = std::max(std::atoi(e), 2);
+  if (const char* e = std::getenv("I7M_ADMM_RANGES"))
+    h->admm_ranges = std::min(std::max(std::atoi(e), 1), (int)i7m_handle::kMaxRanges);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||
@@ -1141,6 +1165,14 @@ void i7m_destroy(i7m_handle* h) {
     if (h->ev_done[c]) (void)hipEventDestroy(h->ev_done[c]);
   }
   if (h->ev_order) (void)hipEventDestroy(h->ev_order);
+  for (int r = 0; r < i7m_handle::kMaxRanges; ++r) {
+    if (h->rs[r]) {
+      (void)hipStreamSynchronize(h->rs[r]);
+      (void)hipStreamDestroy(h->rs[r]);
+    }
+    if (h->ev_rmark[r]) (void)hipEventDestroy(h->ev_rmark[r]);
+    if (h->ev_rdone[r]) (void)hipEventDestroy(h->ev_rdone[r]);
+  }
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
 }
@@ -1278,6 +1310,44 @@ int i7m_synchronize(i7m_handle* h) {
   return I7M_OK;
 }
 
+// ADMM mode: the batch as h->admm_ranges contiguous ranges, each on a stream of its own and
+// started when the range before it has passed its mark (i7m_handle::admm_stagger), every range's
+// end joined back into h->stream.  Results are the one-range solve's: the problems are independent.
+static int solve_admm_staggered(i7m_handle* h, int B, const double* d_xu_in, const double* d_xcur,
+                                const double* d_goals, int goal_stride, double* d_xu_out, ProblemStats* st) {
+  const int R = h->admm_ranges;
+  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+  hipStream_t ss[i7m_handle::kMaxRanges];
+  for (int r = 0; r < R; ++r) {
+    if (r < 2) {
+      ss[r] = h->cs[r];
+    } else {
+      if (!h->rs[r]) HIPCHK(hipStreamCreateWithFlags(&h->rs[r], hipStreamNonBlocking));
+      ss[r] = h->rs[r];
+    }
+    if (!h->ev_rmark[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rmark[r], hipEventDisableTiming));
+    if (!h->ev_rdone[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rdone[r], hipEventDisableTiming));
+  }
+  HIPCHK(hipEventRecord(h->ev_order, h->stream));
+  bool prev_marked = false;
+  for (int r = 0; r < R; ++r) {
+    const long lo = (long)B * r / R, hi = (long)B * (r + 1) / R;
+    HIPCHK(hipStreamWaitEvent(ss[r], h->ev_order, 0));
+    if (prev_marked) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - 1], 0));
+    h->mark_ev = r + 1 < R ? h->ev_rmark[r] : nullptr;
+    const int rc = run_sqp(h, (int)(hi - lo), d_xu_in + lo * T, d_xu_out + lo * T, d_xcur + lo * 12,
+                           d_goals + lo * N * goal_stride, goal_stride, st + lo, lo, ss[r]);
+    prev_marked = r + 1 < R && !h->mark_ev;
+    h->mark_ev = nullptr;
+    if (rc) return rc;
+  }
+  for (int r = 0; r < R; ++r) {
+    HIPCHK(hipEventRecord(h->ev_rdone[r], ss[r]));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_rdone[r], 0));
+  }
+  return I7M_OK;
+}
+
 int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const double* d_xcur, const double* d_goals,
                      int32_t goal_stride, double* d_xu_out, i7m_problem_stats* d_stats) {
   int rc = check_batch(h, B, goal_stride);
@@ -1286,6 +1356,9 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
   HIPCHK(hipSetDevice(h->dev));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
+  if (h->cfg.qp_mode == I7M_QP_ADMM && h->admm_stagger > 0 && h->admm_ranges > 1 && B >= h->admm_stagger_min_b &&
+      h->dev_ranges <= 1)
+    return solve_admm_staggered(h, B, d_xu_in, d_xcur, d_goals, goal_stride, d_xu_out, st);
   if (h->dev_ranges > 1 && B >= h->dev_ranges) {
     // A/B knob (I7M_DEV_RANGES): the batch as contiguous ranges on the two chunk streams, so one
     // range's kernels can fill the SIMDs another range's kernel tail leaves idle

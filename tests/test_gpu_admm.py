@@ -196,6 +196,39 @@ def test_admm_full_size_every_problem_matches_port(lib, model):
     assert rel.max() < 1e-7 and np.median(rel) < 5e-9, (rel.max(), np.median(rel))
 
 
+def test_admm_staggered_device_ranges_equal_one_range(lib, model, monkeypatch):
+    """i7m_solve_device in ADMM mode at B >= 4096 runs the batch as two ranges on streams of their
+    own, the second started behind the first's first scaling + factor (I7M_ADMM_STAGGER 1, the
+    default): two consecutive solves equal a one-range handle's (I7M_ADMM_STAGGER 0) bit for bit,
+    the OSQP state, iteration records, statuses and duals included."""
+    import torch
+    B, N = 4096, 32
+    xcur, goals, XU = synthetic_batch(B, N, 45)
+    dev = torch.device("cuda", 0)
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("I7M_ADMM_STAGGER", mode)
+        h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+        t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
+        outs = []
+        for call in range(2):
+            t_out = torch.empty_like(t_xu)
+            torch.cuda.synchronize()
+            h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr())
+            h.synchronize()
+            outs.append(t_out.cpu().numpy())
+            t_xu = t_out
+        res.append((outs, h.admm_stats(B, with_status=True), h.admm_state(B), h.admm_dual(B)))
+        h.close()
+    (o0, st0, x0, s0), (o1, st1, x1, s1) = res
+    for a, b in zip(o0, o1):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(st0 + x0, st1 + x1):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(s0, s1)
+    assert (st1[0][:, 0] >= 25).all()  # every problem ran its first QP
+
+
 def test_admm_status_and_dual(lib, model):
     """OSQP's result fields through QPSolution: status "solved" with the default settings and
     "maximum iterations reached" when max_iter stops OSQP before its termination test passes; y
