@@ -146,6 +146,7 @@ struct i7m_handle {
   // OSQP iterations after the first termination check) overlap another's stream-bound ones
   // (DESIGN.md §4.7).  0: one range.  I7M_ADMM_STAGGER, I7M_ADMM_RANGES, I7M_ADMM_STAGGER_MIN_B.
   int admm_stagger = 1;
+  int stagger_modes = 1 << I7M_QP_ADMM;  // the QP modes that stagger (bit per mode; I7M_STAGGER_MODES)
   int admm_ranges = 2;
   int admm_stagger_min_b = 4096;  // measured: B = 4096 +17 %; B = 2048 / 1024 -8 / -11 % (two ranges)
   static constexpr int kMaxRanges = 4;
@@ -677,8 +678,19 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
     else
       rc = launch_linearize(h, s, W, P, xin, d_goals, act);
     if (rc) return rc;
+    // the staggered ranges' mark outside ADMM mode (which marks inside its QP): after the first
+    // linearisation (admm_stagger 1) or the first QP (2)
+    const bool mark_here = h->mark_ev && h->cfg.qp_mode != I7M_QP_ADMM;
+    if (mark_here && h->admm_stagger == 1) {
+      HIPCHK(hipEventRecord(h->mark_ev, s));
+      h->mark_ev = nullptr;
+    }
     const double* qsol = nullptr;
     if ((rc = solve_qp(h, s, W, P, xin, d_xs, act, qbuf, &qsol, it))) return rc;
+    if (mark_here && h->mark_ev && h->admm_stagger == 2) {
+      HIPCHK(hipEventRecord(h->mark_ev, s));
+      h->mark_ev = nullptr;
+    }
     // mode 2: the ADMM mode's QP solver carries state, so an alpha = 0 iteration is re-solved
     if ((rc = launch_linesearch(h, s, W, P, xin, d_xu, qsol, d_goals, act, d_st, nullptr, it,
                                 h->cfg.qp_mode == I7M_QP_ADMM ? 2 : 0, h->ablate != 6)))
@@ -1075,6 +1087,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
   if (const char* e = std::getenv("I7M_ADMM_STAGGER")) h->admm_stagger = std::min(std::max(std::atoi(e), 0), 2);
   if (const char* e = std::getenv("I7M_ADMM_STAGGER_MIN_B")) h->admm_stagger_min_b = std::max(std::atoi(e), 2);
+  if (const char* e = std::getenv("I7M_STAGGER_MODES")) h->stagger_modes = std::atoi(e);
   if (const char* e = std::getenv("I7M_ADMM_RANGES"))
     h->admm_ranges = std::min(std::max(std::atoi(e), 1), (int)i7m_handle::kMaxRanges);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
@@ -1356,8 +1369,8 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
   HIPCHK(hipSetDevice(h->dev));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
-  if (h->cfg.qp_mode == I7M_QP_ADMM && h->admm_stagger > 0 && h->admm_ranges > 1 && B >= h->admm_stagger_min_b &&
-      h->dev_ranges <= 1)
+  if (((h->stagger_modes >> h->cfg.qp_mode) & 1) && h->admm_stagger > 0 && h->admm_ranges > 1 &&
+      B >= h->admm_stagger_min_b && h->dev_ranges <= 1)
     return solve_admm_staggered(h, B, d_xu_in, d_xcur, d_goals, goal_stride, d_xu_out, st);
   if (h->dev_ranges > 1 && B >= h->dev_ranges) {
     // A/B knob (I7M_DEV_RANGES): the batch as contiguous ranges on the two chunk streams, so one

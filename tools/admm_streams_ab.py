@@ -1,4 +1,4 @@
-"""A/B: config 3 in ADMM mode as one batch on one stream against K sub-batches on K streams, the
+"""A/B: config 3 in ADMM mode (or --mode box / direct) as one batch on one stream against K sub-batches on K streams, the
 k-th sub-batch started `--offset-us` × k later (a device sleep on its stream), so that one
 sub-batch's latency-bound phases (the factor, the OSQP tail after the first termination check)
 overlap another's stream-bound ones.  Cold OSQP state every step; one JSON line per setting.
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--ks", default="1,2,4")
     ap.add_argument("--offsets", default="0,1000,2000")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--mode", default="admm", choices=["admm", "box", "direct"])
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -43,7 +44,8 @@ def main():
                 b = a.B // K
                 hs, ss, bufs = [], [], []
                 for i in range(K):
-                    h = _lib.Handle(model, N=a.N, max_batch=b, qp_mode=_lib.QP_ADMM)
+                    qm = {"admm": _lib.QP_ADMM, "box": _lib.QP_BOX, "direct": _lib.QP_DIRECT}[a.mode]
+                    h = _lib.Handle(model, N=a.N, max_batch=b, qp_mode=qm)
                     s = torch.cuda.Stream(dev)
                     h.set_stream(s.cuda_stream)
                     xcur, goals, XU = make_batch(h, model, a.B, a.N, seed=45)
@@ -56,7 +58,8 @@ def main():
 
                 def run():
                     for h in hs:
-                        h.admm_reset()
+                        if a.mode == "admm":
+                            h.admm_reset()
                     torch.cuda.synchronize()
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
@@ -79,11 +82,11 @@ def main():
 
                 run()  # warm-up
                 ms = [run() for _ in range(a.steps)]
-                its = np.concatenate([h.admm_stats(b)[0] for h in hs])
+                its = np.concatenate([h.admm_stats(b)[0] for h in hs]) if a.mode == "admm" else np.zeros(1)
                 for h in hs:
                     h.close()
                 used = its[its >= 0]
-                print(json.dumps({"rep": rep, "K": K, "offset_us": off, "B": a.B, "N": a.N,
+                print(json.dumps({"mode": a.mode, "rep": rep, "K": K, "offset_us": off, "B": a.B, "N": a.N,
                                   "ms_per_batch": float(np.mean(ms)), "solves_per_s": a.B / (1e-3 * float(np.mean(ms))),
                                   "osqp_iters_mean": float(used.mean())}), flush=True)
 
