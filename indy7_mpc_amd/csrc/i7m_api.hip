@@ -142,12 +142,13 @@ struct i7m_handle {
   int dev_ranges = 0;  // I7M_DEV_RANGES: i7m_solve_device in this many ranges on the two chunk streams (A/B)
   // ADMM mode, i7m_solve_device with B >= admm_stagger_min_b: the batch as admm_ranges ranges on
   // streams of their own, each started once the one before has passed a mark (1: its first QP's
-  // scaling and factor; 2: its first QP), so one range's latency-bound phases (the factor, the
+  // scaling and factor; 2: its first QP; A/B: 3 its first linearisation, 4 its first scaling), so one range's latency-bound phases (the factor, the
   // OSQP iterations after the first termination check) overlap another's stream-bound ones
   // (DESIGN.md §4.7).  0: one range.  I7M_ADMM_STAGGER, I7M_ADMM_RANGES, I7M_ADMM_STAGGER_MIN_B.
   int admm_stagger = 1;
   int stagger_modes = 1 << I7M_QP_ADMM;  // the QP modes that stagger (bit per mode; I7M_STAGGER_MODES)
   int admm_ranges = 2;
+  int admm_split = 500;  // two ranges: the first's share of the batch, per mille (I7M_ADMM_SPLIT, A/B)
   int admm_stagger_min_b = 4096;  // measured: B = 4096 +17 %; B = 2048 / 1024 -8 / -11 % (two ranges)
   static constexpr int kMaxRanges = 4;
   hipStream_t rs[kMaxRanges] = {};  // ranges 2.. (0 and 1 run on cs[0], cs[1]); created on first use
@@ -549,6 +550,10 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
           hipExtLaunchKernelGGL(k_admm_scale<9>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
         else
           hipExtLaunchKernelGGL(k_admm_scale<18>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
+        if (h->mark_ev && h->admm_stagger == 4) {  // (A/B: the mark between scaling and factor)
+          (void)hipEventRecord(h->mark_ev, s);
+          h->mark_ev = nullptr;
+        }
         hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
       });
       if (rc2) return rc2;
@@ -681,7 +686,7 @@ int run_sqp(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, const dou
     // the staggered ranges' mark outside ADMM mode (which marks inside its QP): after the first
     // linearisation (admm_stagger 1) or the first QP (2)
     const bool mark_here = h->mark_ev && h->cfg.qp_mode != I7M_QP_ADMM;
-    if (mark_here && h->admm_stagger == 1) {
+    if (h->mark_ev && (h->admm_stagger == 3 || (mark_here && h->admm_stagger == 1))) {
       HIPCHK(hipEventRecord(h->mark_ev, s));
       h->mark_ev = nullptr;
     }
@@ -1085,8 +1090,9 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_H2H_TAPER")) h->h2h_taper = std::atoi(e) != 0;
   if (const char* e = std::getenv("I7M_ADMM_CHUNK")) h->admm_chunk = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("I7M_DEV_RANGES")) h->dev_ranges = std::min(std::max(std::atoi(e), 0), 64);
-  if (const char* e = std::getenv("I7M_ADMM_STAGGER")) h->admm_stagger = std::min(std::max(std::atoi(e), 0), 2);
+  if (const char* e = std::getenv("I7M_ADMM_STAGGER")) h->admm_stagger = std::min(std::max(std::atoi(e), 0), 4);
   if (const char* e = std::getenv("I7M_ADMM_STAGGER_MIN_B")) h->admm_stagger_min_b = std::max(std::atoi(e), 2);
+  if (const char* e = std::getenv("I7M_ADMM_SPLIT")) h->admm_split = std::min(std::max(std::atoi(e), 100), 900);
   if (const char* e = std::getenv("I7M_STAGGER_MODES")) h->stagger_modes = std::atoi(e);
   if (const char* e = std::getenv("I7M_ADMM_RANGES"))
     h->admm_ranges = std::min(std::max(std::atoi(e), 1), (int)i7m_handle::kMaxRanges);
@@ -1344,7 +1350,10 @@ static int solve_admm_staggered(i7m_handle* h, int B, const double* d_xu_in, con
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
   bool prev_marked = false;
   for (int r = 0; r < R; ++r) {
-    const long lo = (long)B * r / R, hi = (long)B * (r + 1) / R;
+    auto cut = [&](int q) {
+      return R == 2 && q == 1 ? ((long)B * h->admm_split / 1000 + 3) / 4 * 4 : (long)B * q / R;
+    };
+    const long lo = cut(r), hi = cut(r + 1);
     HIPCHK(hipStreamWaitEvent(ss[r], h->ev_order, 0));
     if (prev_marked) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - 1], 0));
     h->mark_ev = r + 1 < R ? h->ev_rmark[r] : nullptr;
