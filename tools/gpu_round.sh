@@ -37,10 +37,16 @@ if has pmc; then
 fi
 if has admm; then
   # config 3 in ADMM mode (B = 4096, N = 32, cold OSQP state per solve): trace + FETCH / WRITE of k_admm
+  # per kernel over the whole batch (one range: I7M_ADMM_STAGGER=0), then the default schedule's
+  # trace (two staggered ranges of 2048)
+  export I7M_ADMM_STAGGER=0
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/admm_trace -o run -- python $R/tools/profile_kernels.py --admm --steps 2 --warmup 1 > $O/admm_trace.log 2>&1 || { tail -20 $O/admm_trace.log; exit 14; }
   python $R/tools/trace_summary.py $O/admm_trace/run_kernel_trace.csv --batch 4096 --N 32 > $O/admm_trace_summary.json
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/admm_fetch -o fetch -- python $R/tools/profile_kernels.py --admm --steps 1 --warmup 1 > $O/admm_fetch.log 2>&1 || { tail -20 $O/admm_fetch.log; exit 15; }
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/admm_write -o write -- python $R/tools/profile_kernels.py --admm --steps 1 --warmup 1 > $O/admm_write.log 2>&1 || { tail -20 $O/admm_write.log; exit 16; }
+  unset I7M_ADMM_STAGGER
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/admm_trace_st -o run -- python $R/tools/profile_kernels.py --admm --steps 2 --warmup 1 > $O/admm_trace_st.log 2>&1 || { tail -20 $O/admm_trace_st.log; exit 17; }
+  python $R/tools/trace_summary.py $O/admm_trace_st/run_kernel_trace.csv --batch 2048 --N 32 > $O/admm_trace_st_summary.json
 fi
 if has c4; then
   # config 4 (B = 4096, N = 64, box rows): trace + FETCH / WRITE of k_ipm_fused
