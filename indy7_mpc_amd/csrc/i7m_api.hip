@@ -1329,13 +1329,21 @@ int i7m_synchronize(i7m_handle* h) {
   return I7M_OK;
 }
 
-// ADMM mode: the batch as h->admm_ranges contiguous ranges, each on a stream of its own and
-// started when the range before it has passed its mark (i7m_handle::admm_stagger), every range's
-// end joined back into h->stream.  Results are the one-range solve's: the problems are independent.
-static int solve_admm_staggered(i7m_handle* h, int B, const double* d_xu_in, const double* d_xcur,
-                                const double* d_goals, int goal_stride, double* d_xu_out, ProblemStats* st) {
+extern "C++" {  // (C++ helpers inside the C-ABI block)
+// Does a batch of B run as staggered ranges (i7m_handle::admm_stagger)?
+static bool stagger_applies(const i7m_handle* h, int B) {
+  return ((h->stagger_modes >> h->cfg.qp_mode) & 1) && h->admm_stagger > 0 && h->admm_ranges > 1 &&
+         B >= h->admm_stagger_min_b && h->dev_ranges <= 1;
+}
+
+// The batch as h->admm_ranges contiguous ranges, each on a stream of its own and started when
+// the range before it has passed its mark (the first run_sqp of its `body` records it; see
+// i7m_handle::admm_stagger), every range forked from and joined back into h->stream.
+// body(lo, n, stream) enqueues the work of problems [lo, lo + n).  Results are the one-range
+// run's: the problems are independent.
+template <class Body>
+static int run_staggered(i7m_handle* h, int B, Body&& body) {
   const int R = h->admm_ranges;
-  const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
   hipStream_t ss[i7m_handle::kMaxRanges];
   for (int r = 0; r < R; ++r) {
     if (r < 2) {
@@ -1347,18 +1355,17 @@ static int solve_admm_staggered(i7m_handle* h, int B, const double* d_xu_in, con
     if (!h->ev_rmark[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rmark[r], hipEventDisableTiming));
     if (!h->ev_rdone[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rdone[r], hipEventDisableTiming));
   }
+  auto cut = [&](int q) {
+    return R == 2 && q == 1 ? ((long)B * h->admm_split / 1000 + 3) / 4 * 4 : (long)B * q / R;
+  };
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
   bool prev_marked = false;
   for (int r = 0; r < R; ++r) {
-    auto cut = [&](int q) {
-      return R == 2 && q == 1 ? ((long)B * h->admm_split / 1000 + 3) / 4 * 4 : (long)B * q / R;
-    };
     const long lo = cut(r), hi = cut(r + 1);
     HIPCHK(hipStreamWaitEvent(ss[r], h->ev_order, 0));
     if (prev_marked) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - 1], 0));
     h->mark_ev = r + 1 < R ? h->ev_rmark[r] : nullptr;
-    const int rc = run_sqp(h, (int)(hi - lo), d_xu_in + lo * T, d_xu_out + lo * T, d_xcur + lo * 12,
-                           d_goals + lo * N * goal_stride, goal_stride, st + lo, lo, ss[r]);
+    const int rc = body(lo, (int)(hi - lo), ss[r]);
     prev_marked = r + 1 < R && !h->mark_ev;
     h->mark_ev = nullptr;
     if (rc) return rc;
@@ -1369,6 +1376,7 @@ static int solve_admm_staggered(i7m_handle* h, int B, const double* d_xu_in, con
   }
   return I7M_OK;
 }
+}  // extern "C++"
 
 int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const double* d_xcur, const double* d_goals,
                      int32_t goal_stride, double* d_xu_out, i7m_problem_stats* d_stats) {
@@ -1378,9 +1386,13 @@ int i7m_solve_device(i7m_handle* h, int32_t B, const double* d_xu_in, const doub
   if (!d_xu_in || !d_xcur || !d_goals || !d_xu_out) return fail(I7M_EINVAL, "null device pointer");
   HIPCHK(hipSetDevice(h->dev));
   ProblemStats* st = d_stats ? reinterpret_cast<ProblemStats*>(d_stats) : h->d_stats;
-  if (((h->stagger_modes >> h->cfg.qp_mode) & 1) && h->admm_stagger > 0 && h->admm_ranges > 1 &&
-      B >= h->admm_stagger_min_b && h->dev_ranges <= 1)
-    return solve_admm_staggered(h, B, d_xu_in, d_xcur, d_goals, goal_stride, d_xu_out, st);
+  if (stagger_applies(h, B)) {
+    const size_t T = 18 * (size_t)h->cfg.N - 6, N = h->cfg.N;
+    return run_staggered(h, B, [&](long lo, int n, hipStream_t s) {
+      return run_sqp(h, n, d_xu_in + lo * T, d_xu_out + lo * T, d_xcur + lo * 12, d_goals + lo * N * goal_stride,
+                     goal_stride, st + lo, lo, s);
+    });
+  }
   if (h->dev_ranges > 1 && B >= h->dev_ranges) {
     // A/B knob (I7M_DEV_RANGES): the batch as contiguous ranges on the two chunk streams, so one
     // range's kernels can fill the SIMDs another range's kernel tail leaves idle
@@ -1698,16 +1710,30 @@ int i7m_mpc_run(i7m_handle* h, int32_t B, const double* xstart, const double* en
     HIPCHK(hipMemsetAsync(d_gi, 0, 4 * (size_t)B, h->stream));
     HIPCHK(hipMemcpyAsync(d_alive, ones.data(), 4 * (size_t)B, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemsetAsync(h->d_xu, 0, 8 * (size_t)B * T, h->stream));
-    if ((rc2 = run_sqp(h, B, h->d_xu, h->d_xu, h->d_xs, h->d_goal, 3, h->d_stats))) return rc2;
-    for (int i = 0; i < num_steps; ++i) {
-      hipLaunchKernelGGL(k_mpc_goal, dim3((B + 255) / 256), dim3(256), 0, h->stream, h->d_model, B, N, h->d_xs, h->d_goal,
-                         d_ep, n_endpoints, d_gi, d_alive, d_dist + (size_t)i * B);
-      HIPCHK(hipGetLastError());
-      // xu_new = sqp(xcur, goal, XU) into the scratch buffer d_out (XU itself is read only)
-      if ((rc2 = run_sqp(h, B, h->d_xu, h->d_out, h->d_xs, h->d_goal, 3, h->d_stats))) return rc2;
-      hipLaunchKernelGGL(k_mpc_advance, dim3(B), dim3(64), 0, h->stream, h->d_model, B, N, h->cfg.dt, h->d_xs, h->d_xu,
-                         h->d_out, d_alive, d_q + (size_t)i * B * 6);
-      HIPCHK(hipGetLastError());
+    // the instances [lo, lo + n) through every MPC step on stream s (the whole batch on the
+    // handle's stream, or, where the solve staggers, each range on its own: the instances are
+    // independent, so a range runs its steps without waiting for the other)
+    auto loop = [&](long lo, int n, hipStream_t s) -> int {
+      const double* xu0 = h->d_xu + lo * T;
+      double *xu = h->d_xu + lo * T, *out = h->d_out + lo * T, *xs = h->d_xs + lo * 12, *g = h->d_goal + lo * 3 * N;
+      int rc3;
+      if ((rc3 = run_sqp(h, n, xu0, xu, xs, g, 3, h->d_stats + lo, lo, s))) return rc3;
+      for (int i = 0; i < num_steps; ++i) {
+        hipLaunchKernelGGL(k_mpc_goal, dim3((n + 255) / 256), dim3(256), 0, s, h->d_model, n, N, xs, g, d_ep, n_endpoints,
+                           d_gi + lo, d_alive + lo, d_dist + (size_t)i * B + lo);
+        HIPCHK(hipGetLastError());
+        // xu_new = sqp(xcur, goal, XU) into the scratch buffer d_out (XU itself is read only)
+        if ((rc3 = run_sqp(h, n, xu, out, xs, g, 3, h->d_stats + lo, lo, s))) return rc3;
+        hipLaunchKernelGGL(k_mpc_advance, dim3(n), dim3(64), 0, s, h->d_model, n, N, h->cfg.dt, xs, xu, out, d_alive + lo,
+                           d_q + ((size_t)i * B + lo) * 6);
+        HIPCHK(hipGetLastError());
+      }
+      return I7M_OK;
+    };
+    if (stagger_applies(h, B)) {
+      if ((rc2 = run_staggered(h, B, loop))) return rc2;
+    } else if ((rc2 = loop(0, B, h->stream))) {
+      return rc2;
     }
     if (num_steps > 0) {
       if ((rc2 = copy_out(h, dist_out, d_dist, (size_t)num_steps * B))) return rc2;

@@ -229,6 +229,26 @@ def test_admm_staggered_device_ranges_equal_one_range(lib, model, monkeypatch):
     assert (st1[0][:, 0] >= 25).all()  # every problem ran its first QP
 
 
+def test_admm_staggered_closed_loop_equals_one_range(lib, model, monkeypatch):
+    """i7m_mpc_run in ADMM mode at B >= 4096 runs each half of the instances through every MPC
+    step on its own stream (the second half behind the first's first scaling + factor): the
+    distances, q histories, final states and trajectories equal a one-range run's bit for bit
+    (NaN where an instance stopped, in the same places)."""
+    tr = json.load(open(GOLD))["mpc_trace"]
+    B, N = 4096, 32
+    xcur, _, _ = synthetic_batch(B, N, 45)
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("I7M_ADMM_STAGGER", mode)
+        h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+        ends = h.eepos(np.array(tr["endpoint_q"]))
+        res.append(h.mpc_run(xcur, ends, 3))
+        h.close()
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
+    assert np.isfinite(res[1][0][0]).all()
+
+
 def test_admm_status_and_dual(lib, model):
     """OSQP's result fields through QPSolution: status "solved" with the default settings and
     "maximum iterations reached" when max_iter stops OSQP before its termination test passes; y
