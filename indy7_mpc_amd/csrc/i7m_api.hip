@@ -755,8 +755,18 @@ int run_sqp_graphed(i7m_handle* h, int B, const double* d_xu_in, double* d_xu, c
 // chunks of a host-to-host solve of B problems: the handle's setting, else automatic — three
 // (tapered) from 3 072 problems, two from 2 048, one piece below (config 3: 1.42 -> 1.21 ms;
 // at B = 1 024 one piece is fastest; DESIGN.md §5 has the A/B)
+// Does a batch of B run as staggered ranges (i7m_handle::admm_stagger)?
+bool stagger_applies(const i7m_handle* h, int B) {
+  return ((h->stagger_modes >> h->cfg.qp_mode) & 1) && h->admm_stagger > 0 && h->admm_ranges > 1 &&
+         B >= h->admm_stagger_min_b && h->dev_ranges <= 1;
+}
+
+
 int h2h_chunks_for(const i7m_handle* h, int B) {
   if (h->h2h_chunks > 0) return h->h2h_chunks;
+  // ADMM mode where the device solve staggers: two chunks, the second's solve behind the first's
+  // mark (solve_h2h_pipelined_body), i.e. the staggered halves with the copies overlapped
+  if (h->cfg.qp_mode == I7M_QP_ADMM && stagger_applies(h, B)) return 2;
   return B >= 3072 ? 3 : (B >= 2048 ? 2 : 1);
 }
 
@@ -853,15 +863,25 @@ int solve_h2h_pipelined_body(i7m_handle* h, int B, const double* xu_in, const do
     HIPCHK(hipEventRecord(h->ev_in[i], h->cs[0]));
     return I7M_OK;
   };
+  // ADMM mode where the device solve staggers, in two chunks: the second chunk's solve also waits
+  // for the first's mark (its first scaling + factor), as the staggered halves of i7m_solve_device
+  const bool stag = nch == 2 && h->cfg.qp_mode == I7M_QP_ADMM && stagger_applies(h, B);
+  if (stag && !h->ev_rmark[0]) HIPCHK(hipEventCreateWithFlags(&h->ev_rmark[0], hipEventDisableTiming));
+  bool marked0 = false;
   auto solve = [&](int i) -> int {
     const long lo = lo_of(i), n = lo_of(i + 1) - lo;
     const hipStream_t ss = sstream(i);
     HIPCHK(hipStreamWaitEvent(ss, h->ev_in[i], 0));
+    if (stag && i == 1 && marked0) HIPCHK(hipStreamWaitEvent(ss, h->ev_rmark[0], 0));
     double* dxu = h->d_xu + lo * T;
     int r;
-    if (n > 0 && (r = run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
-                              h->d_stats + lo, lo, ss)))
-      return r;
+    h->mark_ev = stag && i == 0 ? h->ev_rmark[0] : nullptr;
+    r = n > 0 ? run_sqp(h, (int)n, dxu, dxu, h->d_xs + lo * 12, h->d_goal + lo * N * goal_stride, goal_stride,
+                        h->d_stats + lo, lo, ss)
+              : I7M_OK;
+    if (stag && i == 0) marked0 = !h->mark_ev;
+    h->mark_ev = nullptr;
+    if (r) return r;
     HIPCHK(hipEventRecord(h->ev_cmp[i], ss));
     return I7M_OK;
   };
@@ -1330,12 +1350,6 @@ int i7m_synchronize(i7m_handle* h) {
 }
 
 extern "C++" {  // (C++ helpers inside the C-ABI block)
-// Does a batch of B run as staggered ranges (i7m_handle::admm_stagger)?
-static bool stagger_applies(const i7m_handle* h, int B) {
-  return ((h->stagger_modes >> h->cfg.qp_mode) & 1) && h->admm_stagger > 0 && h->admm_ranges > 1 &&
-         B >= h->admm_stagger_min_b && h->dev_ranges <= 1;
-}
-
 // The batch as h->admm_ranges contiguous ranges, each on a stream of its own and started when
 // the range before it has passed its mark (the first run_sqp of its `body` records it; see
 // i7m_handle::admm_stagger), every range forked from and joined back into h->stream.

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--chunks", default="1,2,3,4,8")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--pinned", action="store_true", help="inputs and outputs in pinned host memory (torch pin_memory)")
+    ap.add_argument("--mode", default="direct", choices=["direct", "admm"],
+                    help="QP mode; admm: every call from a cold OSQP state (admm_reset outside the timing)")
     a = ap.parse_args()
     import numpy as np
 
@@ -33,7 +35,8 @@ def main():
     model = default_model()
     ref = None
     for nch in [int(c) for c in a.chunks.split(",")]:
-        h = _lib.Handle(model, N=a.N, max_batch=a.batch, h2h_chunks=nch)
+        h = _lib.Handle(model, N=a.N, max_batch=a.batch, h2h_chunks=nch,
+                        qp_mode=_lib.QP_ADMM if a.mode == "admm" else _lib.QP_DIRECT)
         xcur, goals, XU = make_batch(h, model, a.batch, a.N, 45)
         out = st = None
         if a.pinned:
@@ -51,6 +54,8 @@ def main():
             st = st_t.numpy().view(_lib.STATS_DTYPE)
         ts = []
         for i in range(a.reps + 3):
+            if a.mode == "admm":
+                h.admm_reset()
             t0 = time.perf_counter()
             out, st = h.solve(xcur, goals, XU, out=out, stats=st)
             if i >= 3:
@@ -59,7 +64,7 @@ def main():
             ref = (out.copy(), st.copy())
         same = bool(np.array_equal(out, ref[0]) and np.array_equal(st, ref[1]))
         med = statistics.median(ts)
-        print(json.dumps({"h2h_chunks": nch, "pipe": os.environ.get("I7M_H2H_PIPE", "2"), "taper": os.environ.get("I7M_H2H_TAPER", "1"), "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
+        print(json.dumps({"mode": a.mode, "h2h_chunks": nch, "pipe": os.environ.get("I7M_H2H_PIPE", "2"), "taper": os.environ.get("I7M_H2H_TAPER", "1"), "pinned": a.pinned, "batch": a.batch, "N": a.N, "median_ms": 1e3 * med,
                           "host_to_host_solves_per_s": a.batch / med, "min_ms": 1e3 * min(ts),
                           "bit_identical_to_first": same}), flush=True)
         h.close()
