@@ -322,7 +322,7 @@ def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 
     el = float(np.mean(times))
     used = it[it >= 0]
     res = {"workload": f"config3 ADMM: B={B}, N={N}, OSQP's iteration per QP (I7M_QP_ADMM), cold OSQP state each step"
-                       + (", two staggered ranges (i7m_handle::admm_stagger)" if B >= 4096 else ""),
+                       + (", two staggered ranges (i7m_handle::admm_stagger)" if B >= 3072 else ""),
            "value": B / el, "unit": "solves/s", "ms_per_step": 1e3 * el, "steps": steps,
            "osqp_iters_per_qp": {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())},
            "qp_iters_mean": float(st["qp_iters"].mean()), "finite": bool(np.isfinite(out).all()),

@@ -149,7 +149,7 @@ struct i7m_handle {
   int stagger_modes = 1 << I7M_QP_ADMM;  // the QP modes that stagger (bit per mode; I7M_STAGGER_MODES)
   int admm_ranges = 2;
   int admm_split = 500;  // two ranges: the first's share of the batch, per mille (I7M_ADMM_SPLIT, A/B)
-  int admm_stagger_min_b = 4096;  // measured: B = 4096 +17 %; B = 2048 / 1024 -8 / -11 % (two ranges)
+  int admm_stagger_min_b = 3072;  // measured, two ranges: B = 8192 / 4096 / 3072 +9 / +17 / +5 %; 2048 / 1024 -8 / -11 %
   static constexpr int kMaxRanges = 4;
   hipStream_t rs[kMaxRanges] = {};  // ranges 2.. (0 and 1 run on cs[0], cs[1]); created on first use
   hipEvent_t ev_rmark[kMaxRanges] = {}, ev_rdone[kMaxRanges] = {};

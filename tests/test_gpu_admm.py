@@ -197,7 +197,7 @@ def test_admm_full_size_every_problem_matches_port(lib, model):
 
 
 def test_admm_staggered_device_ranges_equal_one_range(lib, model, monkeypatch):
-    """i7m_solve_device in ADMM mode at B >= 4096 runs the batch as two ranges on streams of their
+    """i7m_solve_device in ADMM mode at B >= 3072 runs the batch as two ranges on streams of their
     own, the second started behind the first's first scaling + factor (I7M_ADMM_STAGGER 1, the
     default): two consecutive solves equal a one-range handle's (I7M_ADMM_STAGGER 0) bit for bit,
     the OSQP state, iteration records, statuses and duals included."""
@@ -230,7 +230,7 @@ def test_admm_staggered_device_ranges_equal_one_range(lib, model, monkeypatch):
 
 
 def test_admm_staggered_closed_loop_equals_one_range(lib, model, monkeypatch):
-    """i7m_mpc_run in ADMM mode at B >= 4096 runs each half of the instances through every MPC
+    """i7m_mpc_run in ADMM mode at B >= 3072 runs each half of the instances through every MPC
     step on its own stream (the second half behind the first's first scaling + factor): the
     distances, q histories, final states and trajectories equal a one-range run's bit for bit
     (NaN where an instance stopped, in the same places)."""
