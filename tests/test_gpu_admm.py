@@ -249,6 +249,30 @@ def test_admm_staggered_closed_loop_equals_one_range(lib, model, monkeypatch):
     assert np.isfinite(res[1][0][0]).all()
 
 
+def test_admm_staggered_host_to_host_equals_one_piece(lib, model, monkeypatch):
+    """i7m_solve in ADMM mode at B >= 3072 runs two chunks (copy-in, solve, copy-out each), the
+    second chunk's solve behind the first's first scaling + factor: two consecutive solves equal a
+    one-piece handle's (h2h_chunks = 1, no stagger) bit for bit, state and OSQP records included."""
+    B, N = 3072, 32
+    xcur, goals, XU = synthetic_batch(B, N, 46)
+    monkeypatch.setenv("I7M_ADMM_STAGGER", "0")
+    h1 = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, h2h_chunks=1)
+    monkeypatch.setenv("I7M_ADMM_STAGGER", "1")
+    h2 = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+    a1, s1 = h1.solve(xcur, goals, XU)
+    a2, s2 = h2.solve(xcur, goals, XU)
+    np.testing.assert_array_equal(a1, a2)
+    b1, _ = h1.solve(xcur, goals, a1)
+    b2, _ = h2.solve(xcur, goals, a2)
+    np.testing.assert_array_equal(b1, b2)
+    for u, v in zip(h1.admm_state(B), h2.admm_state(B)):
+        np.testing.assert_array_equal(u, v)
+    for u, v in zip(h1.admm_stats(B, with_status=True), h2.admm_stats(B, with_status=True)):
+        np.testing.assert_array_equal(u, v)
+    h1.close()
+    h2.close()
+
+
 def test_admm_status_and_dual(lib, model):
     """OSQP's result fields through QPSolution: status "solved" with the default settings and
     "maximum iterations reached" when max_iter stops OSQP before its termination test passes; y
