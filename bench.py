@@ -1,7 +1,10 @@
 """Bench: batched SQP-MPC solves/s on MI355X (BASELINE.json metric, config 3: B=4096, N=32).
 
 A "step" = one full SQP_OSQP.sqp solve (<=2 x linearise + QP + line search, src/osqp_sqp.py:76-93)
-of every problem in the per-GPU batch, inputs resident in HBM.  Multi-GPU: one process per GPU
+of every problem in the per-GPU batch, inputs resident in HBM.  The headline (`value`) runs the
+drop-in default QP mode — OSQP's own iteration on the device (I7M_QP_ADMM), the mode that
+reproduces CPU OSQP within north_star's 1e-4 — from a fresh OSQP state every step; the exact KKT
+solve (I7M_QP_DIRECT) is the extra `exact_mode`.  Multi-GPU: one process per GPU
 (torch.distributed.run), each rank solves its own shard (weak scaling, no data-path collective);
 a gloo barrier brackets the timed region and the max time over ranks is reported.  One GPU runs
 config 3 (B = 4096, seed 45); N ranks run config 5 (one global batch of N x 4096, seed 47, a
@@ -78,7 +81,7 @@ def build_native_port():
         return cpu.LIB, f"g++ -O3 -march=x86-64-v3 (native build failed: {e})"
 
 
-def cpu_baseline(N: int, budget_s: float, seed: int, threads: int, native):
+def cpu_baseline_exact(N: int, budget_s: float, seed: int, threads: int, native):
     """The C++ CPU port (oracle/cpp/i7m_cpu.cpp: the same SQP, exact KKT solve) timed on the
     host cores on a bounded sample of the same workload, single-threaded and with `threads`
     OpenMP threads; plus the instrumented flop count of that algorithm on the sample.
@@ -146,14 +149,16 @@ def _cpu_model():
     return "unknown"
 
 
-def _pmc_traffic(kernel: str, B: int, N: int):
+def _pmc_traffic(kernel: str, B: int, N: int, suffix: str = ""):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json,
-    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, x1024) for this kernel/config, if present."""
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, x1024) for this kernel/config, if present.
+    suffix ":stagger": the launches of ADMM mode's staggered ranges (B = problems per launch),
+    averaged over every launch of the step, as the bench's per-launch time is."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(f"{kernel}:B{B}:N{N}")
+        e = d.get(f"{kernel}:B{B}:N{N}{suffix}")
         return None if e is None else e["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         return None
@@ -274,160 +279,51 @@ def admm_bytes_per_iter(N: int):
     return 8 * N * (2 * 300 + 2 * 72 + 48)
 
 
-def config3_admm(model, stream, local: int, steps: int, B: int = 4096, N: int = 32, native=None,
-                 cpu_budget: float = 10.0, cpu_threads: int = 1):
-    """Config 3's problems (B = 4096, N = 32) with the QP solved by OSQP's own algorithm on the
-    device (I7M_QP_ADMM, k_admm_scale / _factor / _iter) — the reference's solver (src/osqp_solver.py:38-40, 137-143).
-    Reported beside the headline (which solves each QP exactly).  Every timed step starts from a
-    fresh OSQP state (i7m_admm_reset outside the timed region, the step itself timed by HIP events
-    on the solve stream): the reference's first solve, its hardest.  With `native` (rank 0, N = 1)
-    it carries `parity_vs_port` (every problem of one cold step against the port's ADMM mode) and
-    `cpu_baseline` (the port's ADMM mode on a bounded sample)."""
-    import torch
-    from indy7_mpc_amd import _lib
-    from indy7_mpc_amd.synthetic import make_batch
-
-    dev = torch.device("cuda", local)
-    h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=_lib.QP_ADMM)
-    h.set_stream(stream.cuda_stream)
-    xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 3)
-    t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
-    t_out = torch.empty_like(t_xu)
-    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-
-    def step():
-        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
-
-    h.admm_reset()
-    step()  # warm-up (kernel load)
-    torch.cuda.synchronize(dev)
-    times, its = [], []
-    h.reset_kernel_times()
-    h.set_timing(True)
-    for _ in range(steps):
-        h.admm_reset()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        step()
-        b.record(stream)
-        torch.cuda.synchronize(dev)
-        times.append(a.elapsed_time(b) / 1e3)
-        its.append(h.admm_stats(B)[0])
-    h.set_timing(False)
-    kt = h.kernel_times()
-    out = t_out.cpu().numpy()
-    st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
-    it = its[-1]
-    h.close()
-    el = float(np.mean(times))
-    used = it[it >= 0]
-    res = {"workload": f"config3 ADMM: B={B}, N={N}, OSQP's iteration per QP (I7M_QP_ADMM), cold OSQP state each step"
-                       + (", two staggered ranges (i7m_handle::admm_stagger)" if B >= 3072 else ""),
-           "value": B / el, "unit": "solves/s", "ms_per_step": 1e3 * el, "steps": steps,
-           "osqp_iters_per_qp": {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())},
-           "qp_iters_mean": float(st["qp_iters"].mean()), "finite": bool(np.isfinite(out).all()),
-           "kernels": {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c} for k, (ms, c) in kt.items()}}
-    if "k_admm_iter" in kt:
-        ms, cnt = kt["k_admm_iter"]
-        avg_s = ms / max(cnt, 1) / 1e3
-        # problems per launch and OSQP iterations per launch (the last step's record)
-        ppl = float((it >= 0).sum()) / max(cnt // steps, 1)
-        ipl = float(used.sum()) / max(cnt // steps, 1)
-        ab = algorithmic_bytes(N)
-        achieved = ppl * ab / avg_s / 1e9
-        stream_gbs = ipl * admm_bytes_per_iter(N) / avg_s / 1e9
-        res["roofline"] = {"bound": "hbm", "kernel": "k_admm_iter", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic("k_admm_iter", B, N),
-                           "algorithmic_bytes_per_problem": ab, "problems_per_launch": ppl,
-                           "avg_launch_us": avg_s * 1e6,
-                           "factor_stream": {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,
-                                             "achieved_GBs": stream_gbs, "frac": stream_gbs / HBM_PEAK_GBS,
-                                             "note": "the blocks every OSQP iteration re-reads (bench.admm_bytes_per_iter)"}}
-        # the same bytes over the whole step (every kernel of both SQP iterations): with the
-        # staggered ranges a launch shares the GPU with the other range's kernels, so its own
-        # duration understates what the stream achieves
-        step_gbs = ipl * (cnt // steps) * admm_bytes_per_iter(N) / el / 1e9
-        res["roofline"]["factor_stream"].update({"step_achieved_GBs": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS})
-    # the reference's use: a closed loop whose every QP warm-starts from the instance's last one
-    res["closed_loop"] = mpc_closed_loop(model, stream, local, B, N, steps=10, qp_mode=_lib.QP_ADMM)
-    if native is not None:
-        from oracle import cpu
-        lib_path, build_desc = native
-        cpu.load(lib_path)
-        stp = cpu.AdmmState(B, N)
-        ref, qp, al, _, rit = cpu.solve_admm(xcur, goals, XU, N, stp, nthreads=cpu_threads)
-        rel = np.linalg.norm(out - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
-        ga = st["alphas"][:, :al.shape[1]]
-        used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
-        used_c = ~np.isnan(al)
-        same_alpha = np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == al, True), axis=1)
-        same_it = np.all(np.where(rit >= 0, it == rit, True), axis=1)
-        res["parity_vs_port"] = {
-            "problems": int(B), "alpha_sequence_agreement": float(same_alpha.mean()),
-            "osqp_iters_agreement": float(same_it.mean()), "qp_iters_agreement": float((st["qp_iters"] == qp).mean()),
-            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
-            "reference": "oracle/cpp/i7m_cpu.cpp ADMM mode (oracle/osqp_admm.py in block form)"}
-        res["parity_vs_osqp"] = {
-            "mode": "ADMM (OSQP's iteration on the device) vs CPU OSQP (the port's ADMM mode, eps 1e-3, cold state)",
-            "problems": int(B), "xu_rel_err_median": float(np.median(rel)), "xu_rel_err_max": float(rel.max()),
-            "share_above_1e-4": float((rel > 1e-4).mean()), "alpha_sequence_agreement": float(same_alpha.mean()),
-            "osqp_iters_agreement": float(same_it.mean()), "meets_north_star_1e-4": bool(rel.max() <= 1e-4)}
-        t0 = time.perf_counter()
-        cpu.solve_admm(xcur[:4], goals[:4], XU[:4], N, cpu.AdmmState(4, N), nthreads=1)
-        per = (time.perf_counter() - t0) / 4
-        n = int(max(4, min(B, cpu_budget / 2 / per)))
-        t0 = time.perf_counter()
-        cpu.solve_admm(xcur[:n], goals[:n], XU[:n], N, cpu.AdmmState(n, N), nthreads=1)
-        t1 = time.perf_counter()
-        nm = min(B, n * cpu_threads)
-        t2 = time.perf_counter()
-        cpu.solve_admm(xcur[:nm], goals[:nm], XU[:nm], N, cpu.AdmmState(nm, N), nthreads=cpu_threads)
-        t3 = time.perf_counter()
-        res["cpu_baseline"] = {
-            "value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"{n} cold ADMM-mode solves (the first {n} of these draws) by oracle/cpp/i7m_cpu.cpp, 1 thread, "
-                      f"{t1 - t0:.1f}s",
-            "build": build_desc,
-            "all_cores": {"value": nm / (t3 - t2), "cores": cpu_threads, "sample": f"{nm} solves, {cpu_threads} threads"}}
-    return res
-
-
 def config2(model, stream, local: int, steps: int, warmup: int, B: int = 64, N: int = 32):
     """a small batch (B = 64, N = 32) on one GPU, device-resident inputs,
-    same step definition as the headline.  At this size every kernel is one partially filled
-    launch, so the figure is set by the per-problem latency of the pipeline, not by throughput;
-    reported beside the headline with its per-step p50 (HIP events on the solve stream)."""
+    the headline's step definition (ADMM mode, a fresh OSQP state every step), with the exact mode
+    beside it.  At this size every kernel is one partially filled launch, so the figure is set by
+    the per-problem latency of the pipeline, not by throughput; per-step p50 by HIP events on the
+    solve stream."""
     import torch
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.synthetic import make_batch
 
     dev = torch.device("cuda", local)
-    h = _lib.Handle(model, N=N, max_batch=B, device_id=local)
-    h.set_stream(stream.cuda_stream)
-    xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 2)
-    t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
-    t_out = torch.empty_like(t_xu)
+    res = {}
+    for name, mode in (("admm", _lib.QP_ADMM), ("exact", _lib.QP_DIRECT)):
+        h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=mode)
+        h.set_stream(stream.cuda_stream)
+        xcur, goals, XU = make_batch(h, model, B, N, seed=42 + 2)
+        t_xu, t_xs, t_g = (torch.from_numpy(x).to(dev) for x in (XU, xcur, goals))
+        t_out = torch.empty_like(t_xu)
 
-    def step():
-        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
+        def step():
+            if mode == _lib.QP_ADMM:
+                h.admm_reset(B)
+            h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    t0 = time.perf_counter()
-    for i in range(steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    out = t_out.cpu().numpy()
-    h.close()
-    return {"workload": f"config2: B={B}, N={N}, full SQP, exact KKT", "value": B * steps / el, "unit": "solves/s",
-            "ms_per_step": 1e3 * el / steps, "steps": steps,
-            "p50_step_ms": statistics.median(a.elapsed_time(b) for a, b in evs),
-            "finite": bool(np.isfinite(out).all())}
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            evs[i][0].record(stream)
+            step()
+            evs[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        out = t_out.cpu().numpy()
+        h.close()
+        r = {"value": B * steps / el, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
+             "p50_step_ms": statistics.median(a.elapsed_time(b) for a, b in evs),
+             "finite": bool(np.isfinite(out).all())}
+        if name == "admm":
+            res.update(workload=f"config2: B={B}, N={N}, full SQP, OSQP's iteration (cold state per step)", **r)
+        else:
+            res["exact_mode"] = dict(workload=f"config2: B={B}, N={N}, full SQP, exact KKT", **r)
+    return res
 
 
 def mpc_closed_loop(model, stream, local: int, B: int = 4096, N: int = 32, steps: int = 20, qp_mode=None):
@@ -513,6 +409,374 @@ def launch_ranks(args, argv) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+class Leg:
+    """One QP mode's timed solve loop on this rank's shard, device-resident inputs.
+
+    A step = one full SQP solve (src/osqp_sqp.py:76-93) of every problem of the shard.  ADMM mode
+    (`cold`): every step starts from a fresh OSQP state — i7m_admm_reset, inside the timed region
+    — i.e. the reference's first solve of each problem (osqp.OSQP() set up, then solve()), its
+    hardest; the warm-started use is the closed loop (mpc_closed_loop)."""
+
+    def __init__(self, h, B, bufs, stream, dev, cold):
+        self.h, self.B, self.bufs, self.stream, self.dev, self.cold = h, B, bufs, stream, dev, cold
+
+    def step(self, B=None):
+        t_xu, t_xs, t_g, t_out, t_st = self.bufs
+        n = self.B if B is None else B
+        if self.cold:
+            self.h.admm_reset(n)
+        self.h.solve_device(n, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3,
+                            t_out.data_ptr(), t_st.data_ptr())
+
+    def timed(self, steps, world, dist, kernel_events):
+        """Barrier + synchronize on both sides of `steps` back-to-back steps; returns (max over ranks
+        of the wall time, this rank's own, per-step event ms (kernel_events pass only))."""
+        import torch
+
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if kernel_events:
+            self.h.reset_kernel_times()
+            self.h.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if kernel_events:
+                evs[i][0].record(self.stream)
+            self.step()
+            if kernel_events:
+                evs[i][1].record(self.stream)
+        torch.cuda.synchronize(self.dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if kernel_events:
+            self.h.set_timing(False)
+        own = el
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, own, ([a.elapsed_time(b) for a, b in evs] if kernel_events else None)
+
+    def stats(self):
+        from indy7_mpc_amd import _lib
+
+        return np.frombuffer(self.bufs[4].cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
+
+    def output(self):
+        return self.bufs[3].cpu().numpy()
+
+    def latency_b1(self, reps):
+        import torch
+
+        lat = []
+        for i in range(reps + 3):
+            torch.cuda.synchronize(self.dev)
+            a = time.perf_counter()
+            self.step(1)
+            torch.cuda.synchronize(self.dev)
+            if i >= 3:
+                lat.append((time.perf_counter() - a) * 1e3)
+        return statistics.median(lat)
+
+    def host_to_host(self, xcur, goals, XU):
+        """numpy in -> H2D + kernels + D2H -> numpy out (i7m_solve), 3 warm-up and 20
+        timed calls, median (ADMM: each call from a fresh OSQP state, the reset inside the call's time)."""
+        h2h = []
+        for i in range(23):
+            a = time.perf_counter()
+            if self.cold:
+                self.h.admm_reset()
+            self.h.solve(xcur, goals, XU)
+            if i >= 3:
+                h2h.append(time.perf_counter() - a)
+        return statistics.median(h2h)
+
+
+def make_leg(model, local, B, N, xcur, goals, XU, stream, qp_mode):
+    import torch
+    from indy7_mpc_amd import _lib
+
+    dev = torch.device("cuda", local)
+    h = _lib.Handle(model, N=N, max_batch=B, device_id=local, qp_mode=qp_mode)
+    h.set_stream(stream.cuda_stream)
+    t_xu, t_xs, t_g = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (XU, xcur, goals))
+    t_out = torch.empty_like(t_xu)
+    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    return Leg(h, B, (t_xu, t_xs, t_g, t_out, t_st), stream, dev, cold=qp_mode == _lib.QP_ADMM)
+
+
+def kernel_summary(ktimes):
+    tot = max(sum(x[0] for x in ktimes.values()), 1e-12)
+    return {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c, "share": ms / tot} for k, (ms, c) in ktimes.items()}
+
+
+def roofline_of(ktimes, steps, problems_per_step, N, traffic):
+    """HBM roofline of the dominant kernel (largest total time): SURVEY.md 8d's 312 N bytes per
+    problem x the problems one launch processes (a step's problem-launches / its launches: later SQP
+    iterations and the staggered ADMM ranges run fewer) / its average launch duration (HIP events
+    on each dispatch, the event pass); traffic = the committed rocprofv3 PMC bytes of that launch."""
+    dom = max(ktimes, key=lambda k: ktimes[k][0])
+    ms, cnt = ktimes[dom]
+    avg_s = ms / max(cnt, 1) / 1e3
+    lps = max(cnt // steps, 1)
+    ppl = float(problems_per_step) / lps
+    ab = algorithmic_bytes(N)
+    achieved = ppl * ab / avg_s / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_over_algorithmic": None if traffic is None else traffic / (ppl * ab),
+            "algorithmic_bytes_per_problem": ab, "algorithmic_source": "SURVEY.md 8d: 312 N B per solve",
+            "problems_per_launch": ppl, "launches_per_step": lps, "avg_launch_us": avg_s * 1e6,
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"}
+
+
+def admm_roofline(ktimes, steps, it, B, N, step_s):
+    """k_admm_iter's roofline: the record of 312 N B per problem per launch, its PMC traffic (the
+    staggered ranges' launch when B >= 3072: profiles/pmc_traffic.json key ':stagger'), and the
+    factor stream every OSQP iteration re-reads (admm_bytes_per_iter) per launch and over the step."""
+    stag = B >= 3072
+    key_b = B // 2 if stag else B
+    traffic = _pmc_traffic("k_admm_iter", key_b, N, ":stagger" if stag else "")
+    ms, cnt = ktimes["k_admm_iter"]
+    r = roofline_of({"k_admm_iter": (ms, cnt)}, steps, float((it >= 0).sum()), N, traffic)
+    avg_s = r["avg_launch_us"] / 1e6
+    ipl = float(it[it >= 0].sum()) / r["launches_per_step"]
+    stream_gbs = ipl * admm_bytes_per_iter(N) / avg_s / 1e9
+    step_gbs = ipl * r["launches_per_step"] * admm_bytes_per_iter(N) / step_s / 1e9
+    r["traffic_key"] = f"k_admm_iter:B{key_b}:N{N}" + (":stagger" if stag else "")
+    r["launch_shape"] = (f"two staggered ranges of {B // 2} problems (i7m_handle::admm_stagger), one launch per "
+                         "range and SQP iteration" if stag else "one range")
+    r["factor_stream"] = {"bytes_per_osqp_iter": admm_bytes_per_iter(N), "osqp_iters_per_launch": ipl,
+                          "achieved_GBs": stream_gbs, "frac": stream_gbs / HBM_PEAK_GBS,
+                          "traffic_over_stream": None if traffic is None else traffic / (ipl * admm_bytes_per_iter(N)),
+                          "step_achieved_GBs": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
+                          "note": "the blocks every OSQP iteration re-reads (bench.admm_bytes_per_iter); step_*: over "
+                                  "the whole step, where the other range's kernels overlap a launch"}
+    return r
+
+
+def alpha_agreement(st, al):
+    ga = st["alphas"][:, :al.shape[1]]
+    used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
+    used_c = ~np.isnan(al)
+    return np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == al, True), axis=1)
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b, axis=1) / np.maximum(np.linalg.norm(b, axis=1), 1e-300)
+
+
+OSQP_PINNING = ("CPU OSQP is the port's ADMM mode (oracle/cpp/i7m_cpu.cpp), the block form of oracle/osqp_admm.py's "
+                "restatement of OSQP; the osqp package is not importable here, so parity with OSQP itself is pinned "
+                "only by the reference notebook's printed closed loop (pin_mpc_indy7.ipynb cell 2: "
+                "tests/test_admm_oracle.py::test_osqp_restatement_reproduces_notebook_closed_loop and "
+                "::test_port_admm_closed_loop_matches_notebook) and is otherwise unpinned")
+
+
+def admm_parity(out, st, it, status, xcur, goals, XU, N, threads):
+    """Every problem of the last timed (cold) step against the port's ADMM mode on the same inputs."""
+    from oracle import cpu
+
+    stp = cpu.AdmmState(len(XU), N)
+    ref, qp, al, _, rit = cpu.solve_admm(xcur, goals, XU, N, stp, nthreads=threads)
+    rel = _rel(out, ref)
+    same_it = np.all(np.where(rit >= 0, it == rit, True), axis=1)
+    same_st = np.all(np.where(stp.status >= 0, status == stp.status, True), axis=1)
+    return {"problems": int(len(XU)), "alpha_sequence_agreement": float(alpha_agreement(st, al).mean()),
+            "osqp_iters_agreement": float(same_it.mean()), "osqp_status_agreement": float(same_st.mean()),
+            "qp_iters_agreement": float((st["qp_iters"] == qp).mean()),
+            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
+            "share_above_1e-4": float((rel > 1e-4).mean()), "meets_north_star_1e-4": bool(rel.max() <= 1e-4),
+            "reference": "oracle/cpp/i7m_cpu.cpp ADMM mode (oracle/osqp_admm.py in block form), cold OSQP state",
+            "osqp_pinning": OSQP_PINNING}
+
+
+def cpu_baseline_admm(xcur, goals, XU, N, budget_s, threads, native):
+    """The port's ADMM mode (the same SQP, each QP by OSQP's iteration from a fresh state) on a
+    bounded sample of these draws, 1 thread and the job's share; beside it the numpy restatement
+    (oracle/osqp_ref.py + oracle/osqp_admm.py: the reference's per-knot Python structure with OSQP
+    restated) on one core, the stand-in for osqp_sqp.py itself."""
+    from oracle import cpu
+    from oracle.osqp_ref import OSQPSolverRef, SQPRef
+
+    lib_path, build_desc = native
+    cpu.load(lib_path)
+    B = len(XU)
+    t0 = time.perf_counter()
+    cpu.solve_admm(xcur[:4], goals[:4], XU[:4], N, cpu.AdmmState(4, N), nthreads=1)
+    per = (time.perf_counter() - t0) / 4
+    n = int(max(4, min(B, budget_s / 2 / per)))
+    t0 = time.perf_counter()
+    cpu.solve_admm(xcur[:n], goals[:n], XU[:n], N, cpu.AdmmState(n, N), nthreads=1)
+    t1 = time.perf_counter()
+    nm = min(B, n * threads)
+    t2 = time.perf_counter()
+    cpu.solve_admm(xcur[:nm], goals[:nm], XU[:nm], N, cpu.AdmmState(nm, N), nthreads=threads)
+    t3 = time.perf_counter()
+    npy_n, t4 = 0, time.perf_counter()
+    while npy_n < 256 and (npy_n < 2 or time.perf_counter() - t4 < budget_s / 4):
+        SQPRef(OSQPSolverRef(N=N, qp="osqp")).sqp(xcur[npy_n], goals[npy_n], XU[npy_n].copy())
+        npy_n += 1
+    t5 = time.perf_counter()
+    return {"value": n / (t1 - t0), "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{n} cold ADMM-mode solves (the first {n} of this step's draws, N={N}) by "
+                      f"oracle/cpp/i7m_cpu.cpp, 1 thread, {t1 - t0:.1f}s",
+            "build": build_desc,
+            "all_cores": {"value": nm / (t3 - t2), "cores": threads, "sample": f"{nm} solves, {threads} OpenMP threads",
+                          "host_cpu_count": os.cpu_count(),
+                          "note": "threads = the CPU share this process may use (affinity / OMP_NUM_THREADS), "
+                                  "not os.cpu_count()"},
+            "numpy_restatement": {"value": npy_n / (t5 - t4), "cores": 1,
+                                  "sample": f"{npy_n} cold solves by oracle/osqp_ref.py with OSQP restated "
+                                            f"(oracle/osqp_admm.py, scipy splu of OSQP's KKT), {t5 - t4:.1f}s"},
+            "cpu_model": _cpu_model()}
+
+
+def exact_mode(model, local, B, N, xcur, goals, XU, stream, steps, warmup, world, dist, native, cpu_budget,
+               cpu_thr, seed, with_extras):
+    """The exact KKT solve (I7M_QP_DIRECT, k_riccati: the optimum OSQP approximates to eps 1e-3)
+    on the same inputs as the headline: its own value (same step definition, max over ranks), its
+    roofline, and on rank 0 at N = 1 its parity (vs the port's exact mode) and its distance from
+    CPU OSQP (parity_vs_port_admm: outside north_star's 1e-4 on ~30 % of problems), its CPU
+    baseline and FP64 rooflines."""
+    from indy7_mpc_amd import _lib
+
+    leg = make_leg(model, local, B, N, xcur, goals, XU, stream, _lib.QP_DIRECT)
+    for _ in range(warmup):
+        leg.step()
+    el, _, _ = leg.timed(steps, world, dist, False)
+    el_ev, _, step_ms = leg.timed(steps, world, dist, True)
+    kt = leg.h.kernel_times()
+    st = leg.stats()
+    out = leg.output()
+    value = B * world * steps / el
+    res = {"workload": f"the headline's problems, each QP solved exactly (I7M_QP_DIRECT, block-tridiagonal Riccati "
+                       f"on fp64 MFMA): B={B} problems/GPU, N={N}",
+           "value": value, "unit": "solves/s", "ms_per_step": 1e3 * el / steps, "steps": steps,
+           "p50_latency_ms": statistics.median(step_ms),
+           "value_during_event_pass": B * world * steps / el_ev, "qp_iters_mean": float(st["qp_iters"].mean()),
+           "kernels": kernel_summary(kt),
+           "roofline": roofline_of(kt, steps, float(st["qp_iters"].sum()), N, None)}
+    dom = res["roofline"]["kernel"]
+    tr = _pmc_traffic(dom, B, N)
+    ppl = res["roofline"]["problems_per_launch"]
+    res["roofline"].update(traffic=tr, traffic_over_algorithmic=None if tr is None else tr / (ppl * algorithmic_bytes(N)),
+                           intermediate_bytes_per_problem=intermediate_bytes(N).get(dom))
+    res["roofline_solve"] = {"bound": "hbm", "achieved": value * algorithmic_bytes(N) / 1e9,
+                             "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                             "frac": value * algorithmic_bytes(N) / 1e9 / (HBM_PEAK_GBS * world)}
+    if with_extras:
+        res["host_to_host_solves_per_s"] = B / leg.host_to_host(xcur, goals, XU)
+    if native is not None:
+        from oracle import cpu as cpu_port
+
+        cb = cpu_baseline_exact(N, cpu_budget, seed, cpu_thr, native)
+        ref_xu, _, ref_al, _ = cpu_port.solve(xcur, goals, XU, N, nthreads=cpu_thr)
+        rel = _rel(out, ref_xu)
+        res["parity_vs_port"] = {"problems": int(B), "alpha_sequence_agreement": float(alpha_agreement(st, ref_al).mean()),
+                                 "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
+                                 "reference": "oracle/cpp/i7m_cpu.cpp exact mode (sparse-LU KKT oracle restated)"}
+        osq, _, osq_al, _, _ = cpu_port.solve_admm(xcur, goals, XU, N, cpu_port.AdmmState(B, N), nthreads=cpu_thr)
+        rel_o = _rel(out, osq)
+        res["parity_vs_port_admm"] = {
+            "mode": "the exact KKT solve vs CPU OSQP (the port's ADMM mode, eps 1e-3, cold state)",
+            "problems": int(B), "xu_rel_err_median": float(np.median(rel_o)),
+            "xu_rel_err_p90": float(np.percentile(rel_o, 90)), "xu_rel_err_p99": float(np.percentile(rel_o, 99)),
+            "xu_rel_err_max": float(rel_o.max()), "share_above_1e-4": float((rel_o > 1e-4).mean()),
+            "alpha_sequence_agreement": float(alpha_agreement(st, osq_al).mean()),
+            "meets_north_star_1e-4": bool(rel_o.max() <= 1e-4),
+            "note": "the exact solve is the optimum OSQP approximates to its eps 1e-3, so it differs from OSQP's "
+                    "iterate by OSQP's own tolerance; the headline (ADMM mode) reproduces CPU OSQP",
+            "osqp_pinning": OSQP_PINNING}
+        fl = cb.pop("flops")
+        fl_dom = {"k_linearize": fl["linearize_per_iter"], "k_riccati": fl["riccati_per_iter"]}.get(dom)
+        if fl_dom is not None:
+            a_tf = ppl * fl_dom / (res["roofline"]["avg_launch_us"] / 1e6) / 1e12
+            res["roofline_fp64"] = {"bound": "fp64", "kernel": dom, "achieved": a_tf, "peak": FP64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": a_tf / FP64_PEAK_TFLOPS, "flops_per_problem": fl_dom}
+        res["solve_fp64"] = {"achieved": value * fl["per_solve_mean"] / 1e12, "unit": "TFLOP/s",
+                             "peak": FP64_PEAK_TFLOPS * world,
+                             "frac": value * fl["per_solve_mean"] / 1e12 / (FP64_PEAK_TFLOPS * world),
+                             "flops_per_solve": fl["per_solve_mean"], "merit_evals_per_solve": fl["merit_evals_mean"]}
+        res["cpu_baseline"] = cb
+    if with_extras:
+        res["mpc_closed_loop"] = mpc_closed_loop(model, stream, local, B, N, steps=20, qp_mode=_lib.QP_DIRECT)
+    leg.h.close()
+    return res
+
+
+def headline_line(*, value, elapsed, steps, warmup, world, B, N, seed, devs, step_ms, ktimes, roofline,
+                  osqp_iters, qp_iters_mean, el_ev, lat_b1_ms=None, h2h_s=None, rank_rows=None):
+    """The ONE JSON line's top level (the headline ADMM leg), from measured numbers; rank 0 adds the
+    parity, CPU baseline and extra objects.  Separate from main() so its keys are testable on CPU
+    (tests/test_sharding.py, world size 2 under gloo)."""
+    out = {
+        "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
+        "value": value,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": 1e3 * elapsed / steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": (f"synthetic (random start/goal states, SURVEY.md §8d, seed {seed}"
+                 + (f": one global batch of {B * world}, contiguous shard per rank)" if world > 1 else ")")),
+        "config": {"workload": (f"config3: B={B} problems/GPU, N={N}" if world == 1 else
+                                f"config5: B={B * world} = {world} x {B} problems, N={N}, sharded one shard per rank")
+                               + ", full SQP (<=2 QP + line search), each QP by OSQP's iteration (I7M_QP_ADMM, the "
+                                 "drop-in default: OSQPSolver / SQP_OSQP / batch_sqp), cold OSQP state every step",
+                   "qp_mode": "admm",
+                   "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)",
+                   "devices_used": sorted(set(devs)), "shared_devices": len(set(devs)) < world,
+                   "osqp_state": "cold: every timed step starts from a fresh OSQP state (i7m_admm_reset inside the "
+                                 "timed region), the reference's first solve of a problem (osqp.OSQP().setup then "
+                                 "solve(), src/osqp_solver.py:38-41,137-143); warm-started solves are the closed "
+                                 "loop's (mpc_closed_loop)",
+                   "value_definition": "device-resident: inputs already in HBM when the timed region starts, "
+                                       "B*world*steps / (max over ranks of the barrier-to-barrier wall time of K "
+                                       "back-to-back solves, each from a fresh OSQP state) -- the task contract's "
+                                       "definition of `value` ('whole-job throughput with inputs already resident in "
+                                       "HBM when the timed region starts ... the PCIe-inclusive rate ... is never "
+                                       "value'); BASELINE.md 4's host-to-host rate (H2D + solve + D2H, median of 20 "
+                                       "calls after 3 warm-up) is host_to_host_solves_per_s, its p50 "
+                                       "p50_latency_h2h_ms; the exact KKT mode is the extra exact_mode"},
+        "p50_latency_ms": statistics.median(step_ms),
+        "p50_latency_definition": "p50_latency_ms: device time per batched step (HIP events on the solve stream, the "
+                                  "OSQP reset included); p50_latency_h2h_ms: BASELINE.md 4's p50 of the host-to-host "
+                                  "batched call; p50_latency_b1_ms: host-to-host B = 1 call (device-resident input)",
+        "kernel_timing": {"pass": "second pass of the same K steps with per-launch HIP events on each kernel's dispatch",
+                          "value_during_event_pass": B * world * steps / el_ev},
+        "qp_iters_mean": qp_iters_mean,
+        "osqp_iters_per_qp": osqp_iters,
+        "kernels": kernel_summary(ktimes),
+        "roofline": roofline,
+        "roofline_solve": {"bound": "hbm", "achieved": value * algorithmic_bytes(N) / 1e9, "peak": HBM_PEAK_GBS * world,
+                           "unit": "GB/s", "frac": value * algorithmic_bytes(N) / 1e9 / (HBM_PEAK_GBS * world),
+                           "bytes_per_solve": algorithmic_bytes(N)},
+    }
+    if lat_b1_ms is not None:
+        out["p50_latency_b1_ms"] = lat_b1_ms
+    if h2h_s is not None:
+        out["p50_latency_h2h_ms"] = 1e3 * h2h_s
+        out["host_to_host_solves_per_s"] = B / h2h_s
+    if world > 1 and rank_rows is not None:
+        out["per_rank"] = per_rank_summary(rank_rows, B, steps)
+    return out
+
+
+def osqp_iter_summary(it):
+    used = it[it >= 0]
+    if not used.size:
+        return {"mean": None, "median": None, "max": None}
+    return {"mean": float(used.mean()), "median": float(np.median(used)), "max": int(used.max())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="ranks = GPUs; without WORLD_SIZE in the environment "
@@ -520,7 +784,7 @@ def main():
     ap.add_argument("--share-devices", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share devices round-robin: a rehearsal of the "
                          "multi-rank path on a small box, reported as such)")
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
     ap.add_argument("--N", type=int, default=32)
@@ -531,8 +795,9 @@ def main():
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 (box QP) extra object")
     ap.add_argument("--config4-steps", type=int, default=3)
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (B=64) extra object")
-    ap.add_argument("--no-admm", action="store_true", help="skip the config-3 ADMM-mode (OSQP) extra object")
-    ap.add_argument("--admm-steps", type=int, default=3)
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-mode (direct KKT) extra object")
+    ap.add_argument("--exact-steps", type=int, default=100)
+    ap.add_argument("--no-closed-loop", action="store_true", help="skip the closed-loop extra objects")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -571,7 +836,6 @@ def main():
         raise SystemExit(f"bench.py: {world} ranks but {ndev} visible device(s); --share-devices rehearses that")
     local = local % ndev
     torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
     from indy7_mpc_amd import _lib
     from indy7_mpc_amd.model import default_model
@@ -581,11 +845,9 @@ def main():
     B, N = args.batch, args.N
     T = 18 * N - 6
     model = default_model()
-    h = _lib.Handle(model, N=N, max_batch=B, device_id=local)
     # a real (non-NULL) torch stream, shared with the library, so torch events bracket our kernels
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.Stream(torch.device("cuda", local))
     torch.cuda.set_stream(stream)
-    h.set_stream(stream.cuda_stream)
     # SURVEY.md §8d seeds = 42 + config index: one GPU runs config 3 (B = 4096, seed 45); N ranks
     # run config 5 (a global batch of N x B problems drawn with seed 47, rank r solving its
     # contiguous shard sharding.shard_range(N B, r, N): 8 x 4096 = B 32768 at N = 8)
@@ -593,221 +855,63 @@ def main():
     lo, hi = shard_range(B * world, rank, world)
     xs_all, qg_all = draw_states(model, B * world, seed)
     xcur, qg = xs_all[lo:hi], qg_all[lo:hi]
-    goals = np.tile(h.eepos(qg), (1, N))
+
+    # the headline: the drop-in default, OSQP's iteration on the device (I7M_QP_ADMM)
+    leg = make_leg(model, local, B, N, xcur, np.zeros((B, 3 * N)), np.zeros((B, T)), stream, _lib.QP_ADMM)
+    goals = np.tile(leg.h.eepos(qg), (1, N))
     XU = np.zeros((B, T))
     XU[:, :12] = xcur
-    t_xu = torch.from_numpy(XU).to(dev)
-    t_xs = torch.from_numpy(xcur).to(dev)
-    t_goal = torch.from_numpy(goals).to(dev)
-    t_out = torch.empty_like(t_xu)
-    t_st = torch.zeros(B * _lib.STATS_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-
-    def step():
-        h.solve_device(B, t_xu.data_ptr(), t_xs.data_ptr(), t_goal.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
-
+    leg.bufs[0].copy_(torch.from_numpy(XU))
+    leg.bufs[2].copy_(torch.from_numpy(goals))
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
-    def timed_pass(kernel_events: bool):
-        # pass 1 (`value`) has nothing on the stream but the solves: event records between steps
-        # cost ~5 % of the step (measured); pass 2 carries the per-step and per-kernel events
-        if kernel_events:
-            h.reset_kernel_times()
-            h.set_timing(True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            if kernel_events:
-                evs[i][0].record(stream)
-            step()
-            if kernel_events:
-                evs[i][1].record(stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if kernel_events:
-            h.set_timing(False)
-        own = el
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el, own
-
-    # pass 1: `value` — nothing but the solves between the barriers
-    elapsed, own_el = timed_pass(False)
-    # pass 2: the same K steps with per-step events (p50) and per-launch start/stop events on
-    # each kernel's dispatch (hipExtLaunchKernelGGL): per-kernel durations for the roofline
-    elapsed_ev, _ = timed_pass(True)
-    step_ms = [a.elapsed_time(b) for a, b in evs]
-    ktimes = h.kernel_times()
-
-    # iterations actually run (active problems shrink after a break)
-    st = np.frombuffer(t_st.cpu().numpy().tobytes(), dtype=_lib.STATS_DTYPE)
-    qp_iters_mean = float(st["qp_iters"].mean())
-
-    # B=1 latency (host-to-host, device-resident input)
-    lat = []
-    for i in range(args.latency_reps + 3):
-        torch.cuda.synchronize(dev)
-        a = time.perf_counter()
-        h.solve_device(1, t_xu.data_ptr(), t_xs.data_ptr(), t_goal.data_ptr(), 3, t_out.data_ptr(), t_st.data_ptr())
-        torch.cuda.synchronize(dev)
-        if i >= 3:
-            lat.append((time.perf_counter() - a) * 1e3)
-
-    # host-to-host rate (numpy in -> H2D + kernels + D2H -> numpy out, i7m_solve): the PCIe-
-    # inclusive figure of DESIGN.md §5, never `value`
-    h2h = []
-    for i in range(23):  # 3 warm-up, >= 20 timed, median
-        a = time.perf_counter()
-        h.solve(xcur, goals, XU)
-        if i >= 3:
-            h2h.append(time.perf_counter() - a)
-
-    # the devices the ranks actually ran on (a --share-devices rehearsal puts several on one), and
-    # each rank's own elapsed time and host-to-host rate (rank imbalance and PCIe contention show
-    # on the first real multi-GPU run)
-    rank_rows = gather_rank_rows(dist if world > 1 else None, local, own_el, B / statistics.median(h2h))
+        leg.step()
+    torch.cuda.synchronize()
+    # pass 1: `value` — nothing but the steps between the barriers
+    elapsed, own_el, _ = leg.timed(args.steps, world, dist, False)
+    # pass 2: the same K steps with per-step events (p50) and per-launch start/stop events on each
+    # kernel's dispatch (hipExtLaunchKernelGGL): per-kernel durations for the roofline
+    el_ev, _, step_ms = leg.timed(args.steps, world, dist, True)
+    ktimes = leg.h.kernel_times()
+    st = leg.stats()
+    out_xu = leg.output()
+    it, _, status = leg.h.admm_stats(B, with_status=True)
+    lat_b1 = leg.latency_b1(args.latency_reps)
+    h2h_s = leg.host_to_host(xcur, goals, XU)
+    rank_rows = gather_rank_rows(dist if world > 1 else None, local, own_el, B / h2h_s)
     devs = [int(r[0]) for r in rank_rows]
-
+    value = B * world * args.steps / elapsed
+    roof = admm_roofline(ktimes, args.steps, it, B, N, elapsed / args.steps)
+    line = headline_line(value=value, elapsed=elapsed, steps=args.steps, warmup=args.warmup, world=world, B=B, N=N,
+                         seed=seed, devs=devs, step_ms=step_ms, ktimes=ktimes, roofline=roof,
+                         osqp_iters=osqp_iter_summary(it), qp_iters_mean=float(st["qp_iters"].mean()), el_ev=el_ev,
+                         lat_b1_ms=lat_b1, h2h_s=h2h_s, rank_rows=rank_rows)
+    line["finite"] = bool(np.isfinite(out_xu).all())
+    leg.h.close()
+    # the exact mode on the same shard (every rank: its value is a max over ranks too)
+    ex = None if args.no_exact else exact_mode(model, local, B, N, xcur, goals, XU, stream, args.exact_steps,
+                                               args.warmup, world, dist, native, args.cpu_budget, args.cpu_threads,
+                                               seed, with_extras=(world == 1 and not args.no_closed_loop))
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
-
-    total = B * world * args.steps
-    value = total / elapsed
-    ab = algorithmic_bytes(N)
-    dom = max(ktimes, key=lambda k: ktimes[k][0])
-    dom_ms, dom_cnt = ktimes[dom]
-    dom_avg_s = dom_ms / max(dom_cnt, 1) / 1e3
-    # problems a launch actually processes: iteration 2 only runs the problems still active
-    launches_per_step = max(dom_cnt // args.steps, 1)
-    problems_per_launch = float(st["qp_iters"].sum()) / launches_per_step
-    achieved = problems_per_launch * ab / dom_avg_s / 1e9
-    traffic = _pmc_traffic(dom, B, N)
-    alg_per_launch = problems_per_launch * ab
-    per_kernel = {k: {"avg_us": 1e3 * ms / max(c, 1), "launches": c,
-                      "share": ms / max(sum(x[0] for x in ktimes.values()), 1e-12)} for k, (ms, c) in ktimes.items()}
-    cpu = None if native is None else cpu_baseline(N, args.cpu_budget, seed, args.cpu_threads, native)
-    c4 = None if (args.no_config4 or world > 1) else config4(model, stream, local, args.config4_steps, 1,
-                                                            native=native, cpu_threads=args.cpu_threads)
-    ca = None if (args.no_admm or world > 1) else config3_admm(model, stream, local, args.admm_steps, B, N,
-                                                               native=native, cpu_threads=args.cpu_threads)
-    c2 = None if (args.no_config2 or world > 1) else config2(model, stream, local, 200, 10)
-    mpc = None if (args.no_config2 or world > 1) else mpc_closed_loop(model, stream, local, B, N)
-    out = {
-        "metric": "SQP-MPC solves/sec (Indy7 6-DOF, N=32)",
-        "value": value,
-        "unit": "solves/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": (f"synthetic (random start/goal states, SURVEY.md §8d, seed {seed}"
-                 + (f": one global batch of {B * world}, contiguous shard per rank)" if world > 1 else ")")),
-        "config": {"workload": (f"config3: B={B} problems/GPU, N={N}" if world == 1 else
-                                f"config5: B={B * world} = {world} x {B} problems, N={N}, sharded one shard per rank")
-                               + ", full SQP (<=2 QP + line search), exact KKT",
-                   "batch_per_gpu": B, "N": N, "global_batch": B * world, "parallelism": f"shard{world} (no collective)",
-                   "devices_used": sorted(set(devs)), "shared_devices": len(set(devs)) < world,
-                   "value_definition": "device-resident: inputs already in HBM when the timed region starts, "
-                                       "B*world*steps / (max over ranks of the barrier-to-barrier wall time of K "
-                                       "back-to-back solves) -- the task contract's definition of `value` (measurement "
-                                       "section: 'value is whole-job throughput with inputs already resident in HBM "
-                                       "when the timed region starts ... the PCIe-inclusive rate ... is never value'); "
-                                       "BASELINE.md 4's host-to-host rate (H2D + solve + D2H, median of 20 calls after "
-                                       "3 warm-up) is host_to_host_solves_per_s, its p50 p50_latency_h2h_ms"},
-        "p50_latency_ms": statistics.median(step_ms),
-        "p50_latency_definition": "p50_latency_ms: device time per batched step (HIP events on the solve stream); "
-                                  "p50_latency_h2h_ms: BASELINE.md 4's p50 of the host-to-host batched call; "
-                                  "p50_latency_b1_ms: host-to-host B = 1 call (device-resident input)",
-        "p50_latency_h2h_ms": 1e3 * statistics.median(h2h),
-        "kernel_timing": {"pass": "second pass of the same K steps with per-launch HIP events on each kernel's dispatch",
-                          "value_during_event_pass": B * world * args.steps / elapsed_ev},
-        "p50_latency_b1_ms": statistics.median(lat),
-        "host_to_host_solves_per_s": B / statistics.median(h2h),
-        "qp_iters_mean": qp_iters_mean,
-        "kernels": per_kernel,
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "traffic_over_algorithmic": None if traffic is None else traffic / alg_per_launch,
-                     "algorithmic_bytes_per_problem": ab, "algorithmic_source": "SURVEY.md 8d: 312 N B per solve",
-                     "problems_per_launch": problems_per_launch, "avg_launch_us": dom_avg_s * 1e6,
-                     "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)",
-                     "intermediate_bytes_per_problem": intermediate_bytes(N).get(dom)},
-        "roofline_solve": {"bound": "hbm", "achieved": value * ab / 1e9, "peak": HBM_PEAK_GBS * world,
-                           "unit": "GB/s", "frac": value * ab / 1e9 / (HBM_PEAK_GBS * world),
-                           "bytes_per_solve": ab},
-    }
-    if world > 1:
-        out["per_rank"] = per_rank_summary(rank_rows, B, args.steps)
-    if cpu is not None:
-        # parity at bench scale: the C++ port on exactly the GPU's inputs (all B problems of
-        # this rank), against the last timed step's output and stats
-        from oracle import cpu as cpu_port
-
-        gpu_xu = t_out.cpu().numpy()
-        ref_xu, _, ref_alphas, _ = cpu_port.solve(xcur, goals, XU, N, nthreads=args.cpu_threads)
-        rel = np.linalg.norm(gpu_xu - ref_xu, axis=1) / np.maximum(np.linalg.norm(ref_xu, axis=1), 1e-300)
-        ga = st["alphas"][:, :ref_alphas.shape[1]]
-        used_g = np.arange(ga.shape[1])[None, :] < st["n_alphas"][:, None]
-        used_c = ~np.isnan(ref_alphas)
-        same_alpha = np.all(used_g == used_c, axis=1) & np.all(np.where(used_g, ga == ref_alphas, True), axis=1)
-        cpu["parity_vs_port"] = {
-            "problems": int(B), "alpha_sequence_agreement": float(same_alpha.mean()),
-            "xu_rel_err_max": float(rel.max()), "xu_rel_err_median": float(np.median(rel)),
-            "gate": "SURVEY.md 8d: end-to-end XU rel. err <= 1e-4, alpha agreement reported separately"}
-        # north_star's gate: this line's mode (the exact KKT solve) against CPU OSQP — the port's
-        # ADMM mode (oracle/osqp_admm.py's OSQP restatement in block form, pinned to the reference
-        # notebook's printed closed loop), cold OSQP state, on exactly these inputs
-        osq, _, osq_al, _, _ = cpu_port.solve_admm(xcur, goals, XU, N, cpu_port.AdmmState(B, N), nthreads=args.cpu_threads)
-        rel_o = np.linalg.norm(gpu_xu - osq, axis=1) / np.maximum(np.linalg.norm(osq, axis=1), 1e-300)
-        used_o = ~np.isnan(osq_al)
-        same_o = np.all(used_g == used_o, axis=1) & np.all(np.where(used_g, ga == osq_al, True), axis=1)
-        out["parity_vs_osqp"] = {
-            "mode": "this line's QP mode (direct: exact KKT) vs CPU OSQP (port ADMM mode, eps 1e-3, cold state)",
-            "problems": int(B), "xu_rel_err_median": float(np.median(rel_o)),
-            "xu_rel_err_p90": float(np.percentile(rel_o, 90)), "xu_rel_err_p99": float(np.percentile(rel_o, 99)),
-            "xu_rel_err_max": float(rel_o.max()), "share_above_1e-4": float((rel_o > 1e-4).mean()),
-            "alpha_sequence_agreement": float(same_o.mean()),
-            "meets_north_star_1e-4": bool(rel_o.max() <= 1e-4),
-            "note": "the exact solve is the optimum OSQP approximates to its eps 1e-3, so it differs from OSQP's "
-                    "iterate by OSQP's own tolerance; the mode that reproduces CPU OSQP is config3_admm "
-                    "(its parity_vs_osqp: every problem)"}
-        fl = cpu.pop("flops")
-        fl_dom = {"k_linearize": fl["linearize_per_iter"], "k_riccati": fl["riccati_per_iter"]}.get(dom)
-        if fl_dom is not None:
-            a_tf = problems_per_launch * fl_dom / dom_avg_s / 1e12
-            out["roofline_fp64"] = {"bound": "fp64", "kernel": dom, "achieved": a_tf, "peak": FP64_PEAK_TFLOPS,
-                                    "unit": "TFLOP/s", "frac": a_tf / FP64_PEAK_TFLOPS,
-                                    "flops_per_problem": fl_dom}
-        out["solve_fp64"] = {"achieved": value * fl["per_solve_mean"] / 1e12, "unit": "TFLOP/s",
-                             "peak": FP64_PEAK_TFLOPS * world,
-                             "frac": value * fl["per_solve_mean"] / 1e12 / (FP64_PEAK_TFLOPS * world),
-                             "flops_per_solve": fl["per_solve_mean"], "merit_evals_per_solve": fl["merit_evals_mean"]}
-        out["cpu_baseline"] = cpu
-    if c2 is not None:
-        out["config2"] = c2
-    if c4 is not None:
-        out["config4"] = c4
-    if ca is not None:
-        out["config3_admm"] = ca
-    if mpc is not None:
-        out["mpc_closed_loop"] = mpc
-    print(json.dumps(out), flush=True)
+    if native is not None:
+        line["parity_vs_port"] = admm_parity(out_xu, st, it, status, xcur, goals, XU, N, args.cpu_threads)
+        line["cpu_baseline"] = cpu_baseline_admm(xcur, goals, XU, N, args.cpu_budget / 2, args.cpu_threads, native)
+    if ex is not None:
+        line["exact_mode"] = ex
+    if world == 1:
+        if not args.no_closed_loop:
+            # the reference's use (MPC_OSQP.run_mpc, batched): every QP warm-starts from the
+            # instance's previous one
+            line["mpc_closed_loop"] = mpc_closed_loop(model, stream, local, B, N, steps=10, qp_mode=_lib.QP_ADMM)
+        if not args.no_config2:
+            line["config2"] = config2(model, stream, local, 200, 10)
+        if not args.no_config4:
+            line["config4"] = config4(model, stream, local, args.config4_steps, 1, native=native,
+                                      cpu_threads=args.cpu_threads)
+    print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -76,7 +76,8 @@ extern "C" {
 #define I7M_MAX_N 64
 
 /* ABI revision, returned by i7m_abi_version(); bumped whenever an existing signature, struct
- * layout, field meaning or enum count changes.  5: i7m_get_admm_status and i7m_get_admm_dual
+ * layout, field meaning or enum count changes.  6: i7m_get_admm_status has the value 2 ("solved
+ * inaccurate") and, after admm_max_iter, runs OSQP's closing tests (0.6 builds).  5: i7m_get_admm_status and i7m_get_admm_dual
  * (appended); i7m_get_admm_stats' iteration record is reset to -1 at the start of every solve
  * (0.5 builds).  4: I7M_QP_ADMM and i7m_config's admm_* fields
  * (appended), I7M_K_COUNT 10 (I7M_K_ADMM, I7M_K_ADMM_PREP), i7m_admm_reset / i7m_get_admm_stats /
@@ -86,7 +87,7 @@ extern "C" {
  * 2: i7m_aba / i7m_rk4 take a wrench `frame` before their outputs and i7m_set_external_wrench a
  * trailing `frame` (0.2 builds); 1 had neither.  A caller built against another revision must not
  * call through this library: compare first. */
-#define I7M_ABI_VERSION 5
+#define I7M_ABI_VERSION 6
 
 #define I7M_OK 0
 #define I7M_EINVAL -1   /* bad argument (size, null pointer, unsupported N) */
@@ -260,10 +261,12 @@ int i7m_get_admm_stats(i7m_handle* h, int32_t B, int32_t* iters, double* rho);
 /* I7M_QP_ADMM: the carried OSQP state of problems [0, B) in OSQP's scaled coordinates: x (B, T),
  * z, y (B, 12N), the previous QP's linear cost, unscaled (B, T), rho (B).  Any may be NULL. */
 int i7m_get_admm_state(i7m_handle* h, int32_t B, double* x, double* z, double* y, double* q, double* rho);
-/* I7M_QP_ADMM (ABI 5): OSQP's result status of every SQP iteration's QP in the last solve
- * (B, I7M_MAX_SQP): 1 its termination test passed ("solved"), 0 admm_max_iter was reached
- * first ("maximum iterations reached"), -1 the problem ran no QP at that iteration.  The
- * reference's solve() returns it in .info.status (src/osqp_solver.py:143). */
+/* I7M_QP_ADMM (ABI 6): OSQP's result status of every SQP iteration's QP in the last solve
+ * (B, I7M_MAX_SQP): 1 "solved" (its termination test passed), 2 "solved inaccurate" and 0
+ * "maximum iterations reached" (admm_max_iter came first: as OSQP, the test is run once more at
+ * the final iterate unless the last iteration ran it, then with eps_abs and eps_rel x 10, which
+ * gives 2), -1 the problem ran no QP at that iteration.  The reference's solve() returns it in
+ * .info.status (src/osqp_solver.py:143). */
 int i7m_get_admm_status(i7m_handle* h, int32_t B, int32_t* status);
 /* I7M_QP_ADMM (ABI 5): the dual y of each problem's last QP, unscaled as OSQP returns it in
  * result.y (y = E y_s / c: the carried scaled y with that QP's row scaling E and cost scale c),

@@ -20,7 +20,7 @@ import numpy as np
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("I7M_LIB", os.path.join(LIB_DIR, "libindy7mpc.so"))  # I7M_LIB: A/B builds
 
-ABI_VERSION = 5  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
+ABI_VERSION = 6  # I7M_ABI_VERSION of include/indy7_mpc.h this binding's SIGNATURES follow
 NJ, NX, NU = 6, 12, 6
 MAX_SQP = 8
 MAX_N = 64
@@ -335,7 +335,7 @@ class Handle:
 
     def admm_stats(self, B, with_status=False):
         """I7M_QP_ADMM: (OSQP iterations per SQP iteration of the last solve (B, 8), -1 = none;
-        rho (B,)); with_status also OSQP's status per SQP iteration (B, 8): 1 solved, 0 maximum
+        rho (B,)); with_status also OSQP's status per SQP iteration (B, 8): 1 solved, 2 solved inaccurate, 0 maximum
         iterations reached, -1 no QP."""
         it = np.zeros((B, MAX_SQP), dtype=np.int32)
         rho = np.zeros(B)

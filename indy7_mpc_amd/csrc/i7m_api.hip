@@ -954,6 +954,8 @@ int drain_after_error(i7m_handle* h, int rc) {
   for (int c = 0; c < 2; ++c)
     if (h->cs[c]) (void)hipStreamSynchronize(h->cs[c]);
   if (h->cs2) (void)hipStreamSynchronize(h->cs2);
+  for (int r = 2; r < i7m_handle::kMaxRanges; ++r)  // the staggered ranges' own streams
+    if (h->rs[r]) (void)hipStreamSynchronize(h->rs[r]);
   (void)hipStreamSynchronize(h->stream);
   g_err = msg;
   return rc;
@@ -1369,20 +1371,37 @@ static int run_staggered(i7m_handle* h, int B, Body&& body) {
     if (!h->ev_rmark[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rmark[r], hipEventDisableTiming));
     if (!h->ev_rdone[r]) HIPCHK(hipEventCreateWithFlags(&h->ev_rdone[r], hipEventDisableTiming));
   }
+  // range boundaries, clamped to [0, B] (the rounded split of a small B or an extreme
+  // I7M_ADMM_SPLIT must not run past the batch); an empty range is skipped
   auto cut = [&](int q) {
-    return R == 2 && q == 1 ? ((long)B * h->admm_split / 1000 + 3) / 4 * 4 : (long)B * q / R;
+    const long c = R == 2 && q == 1 ? ((long)B * h->admm_split / 1000 + 3) / 4 * 4 : (long)B * q / R;
+    return std::min<long>(std::max<long>(c, 0), B);
   };
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
   bool prev_marked = false;
   for (int r = 0; r < R; ++r) {
     const long lo = cut(r), hi = cut(r + 1);
     HIPCHK(hipStreamWaitEvent(ss[r], h->ev_order, 0));
+    if (hi <= lo) {
+      prev_marked = false;
+      continue;
+    }
     if (prev_marked) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - 1], 0));
     h->mark_ev = r + 1 < R ? h->ev_rmark[r] : nullptr;
     const int rc = body(lo, (int)(hi - lo), ss[r]);
     prev_marked = r + 1 < R && !h->mark_ev;
     h->mark_ev = nullptr;
-    if (rc) return rc;
+    if (rc) {
+      // join the ranges already started back into h->stream before the error returns:
+      // the caller's cleanup after a synchronize of h->stream must not race them
+      const std::string msg = g_err;
+      for (int q = 0; q <= r; ++q) {
+        (void)hipEventRecord(h->ev_rdone[q], ss[q]);
+        (void)hipStreamWaitEvent(h->stream, h->ev_rdone[q], 0);
+      }
+      g_err = msg;
+      return rc;
+    }
   }
   for (int r = 0; r < R; ++r) {
     HIPCHK(hipEventRecord(h->ev_rdone[r], ss[r]));

@@ -29,18 +29,30 @@ from scipy.sparse import bmat, csc_matrix, triu
 from . import _lib
 
 
+# i7m_get_admm_status values -> OSQP's (status, status_val)
+ADMM_STATUS = {1: ("solved", 1), 2: ("solved inaccurate", 2), 0: ("maximum iterations reached", -2)}
+
+
 class QPSolution:
     """What ``osqp.OSQP().solve()`` returns: ``.x`` (the only field the reference reads,
     src/osqp_solver.py:143, src/osqp_sqp.py:80), ``.y`` and ``.info.status`` / ``.info.iter``.
-    ADMM mode: OSQP's status string ("solved", or "maximum iterations reached" when the
-    termination test never passed within max_iter), its iteration count and the unscaled dual
-    y = E y_s / c.  Direct mode: the exact KKT solve ("solved", 0 iterations, y None)."""
+    ADMM mode: OSQP's status string ("solved"; "solved inaccurate" or "maximum iterations
+    reached" when the termination test never passed within max_iter), its iteration count and the
+    unscaled dual y = E y_s / c.  Direct mode: the exact KKT solve ("solved", 0 iterations, y None)."""
 
     def __init__(self, x, status="solved", iters=0, y=None):
         self.x = x
         self.y = y
-        self.info = type("info", (), {"status": status, "iter": iters,
-                                      "status_val": 1 if status == "solved" else -2})()
+        val = {s: v for s, v in ADMM_STATUS.values()}[status]
+        self.info = type("info", (), {"status": status, "iter": iters, "status_val": val})()
+
+    @classmethod
+    def from_admm(cls, x, code, iters, y):
+        """From i7m_get_admm_status's code; -1 (no QP ran) is an error, not "solved"."""
+        code = int(code)
+        if code not in ADMM_STATUS:
+            raise RuntimeError(f"no OSQP result for this QP (status code {code})")
+        return cls(x, status=ADMM_STATUS[code][0], iters=int(iters), y=y)
 
 
 class OSQPSolver:
@@ -141,8 +153,7 @@ class OSQPSolver:
         if self.box["qp_mode"] == _lib.QP_ADMM:
             its, _, solved = self.handle.admm_stats(1, with_status=True)
             y = self.handle.admm_dual(1)[0]
-            sol = QPSolution(x, status="solved" if solved[0, 0] else "maximum iterations reached",
-                             iters=int(its[0, 0]), y=y)
+            sol = QPSolution.from_admm(x, solved[0, 0], its[0, 0], y)
         else:
             sol = QPSolution(x)
         self._pending_A = (xu, xs)

@@ -289,6 +289,35 @@ void forward_dynamics(const Model& Md, const R* c, const R* s, const R* v, const
   chol6_solve(L, a);
 }
 
+// World-frame wrench [f; n] about the world origin -> joint 6's local frame at (c, s) = cos / sin(q):
+// data.oMi[6].actInv (src/gato_mpc_batch_sample.py:151-161): f_l = R' f, n_l = R' (n - p x f)
+template <class R>
+void wrench_world_to_local(const Model& Md, const R* c, const R* s, const double* fw, double* fl) {
+  double Rw[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, p[3] = {0, 0, 0};
+  for (int i = 0; i < 6; ++i) {
+    const double* Rp = Md.Rp[i];
+    const double* t = Md.tp[i];
+    const double ci = val(c[i]), si = val(s[i]);
+    double np_[3], RR[3][3];
+    for (int r = 0; r < 3; ++r) np_[r] = p[r] + Rw[r][0] * t[0] + Rw[r][1] * t[1] + Rw[r][2] * t[2];
+    for (int r = 0; r < 3; ++r)
+      for (int q = 0; q < 3; ++q) RR[r][q] = Rw[r][0] * Rp[q] + Rw[r][1] * Rp[3 + q] + Rw[r][2] * Rp[6 + q];
+    for (int r = 0; r < 3; ++r) {
+      Rw[r][0] = RR[r][0] * ci + RR[r][1] * si;
+      Rw[r][1] = RR[r][1] * ci - RR[r][0] * si;
+      Rw[r][2] = RR[r][2];
+      p[r] = np_[r];
+    }
+  }
+  const double m0 = fw[3] - (p[1] * fw[2] - p[2] * fw[1]);
+  const double m1 = fw[4] - (p[2] * fw[0] - p[0] * fw[2]);
+  const double m2 = fw[5] - (p[0] * fw[1] - p[1] * fw[0]);
+  for (int q = 0; q < 3; ++q) {
+    fl[q] = Rw[0][q] * fw[0] + Rw[1][q] * fw[1] + Rw[2][q] * fw[2];
+    fl[3 + q] = Rw[0][q] * m0 + Rw[1][q] * m1 + Rw[2][q] * m2;
+  }
+}
+
 template <class R>
 void fk_jac(const Model& Md, const R* c, const R* s, R* p, R J[3][6]) {
   R Rw[3][3] = {{R(1), R(0), R(0)}, {R(0), R(1), R(0)}, {R(0), R(0), R(1)}};
@@ -321,6 +350,11 @@ void fk_jac(const Model& Md, const R* c, const R* s, R* p, R J[3][6]) {
 
 struct Params {
   int N, regularize, max_iters, goal_stride;
+  // external wrench frame: 0 = constant in joint 6's frame (pinocchio f_ext), 1 = a WORLD-frame
+  // spatial force about the world origin, as batch_sqp's callers give it (gato_controller.py:
+  // 77-81,120-129), converted per configuration by oMi[6].actInv (src/gato_mpc_batch_sample.py:
+  // 151-161) — the GPU's I7M_WRENCH_WORLD (i7m_dynamics.h wrench_world_to_local)
+  int fext_world;
   double dt, dQ, R, QN, eps, mu, step_tol;
   // config 4 box rows (oracle/box_ipm.py; 0 = the reference's equality-only QP)
   int box_mask, box_max_iters;
@@ -459,7 +493,10 @@ struct Solver {
         imul(m, h[i], Ib[i], A0[i], IA);
         fcross(V[i], hV[i], VxH);
         for (int r = 0; r < 6; ++r) F0[i][r] = IA[r] + VxH[r];
-        if (f6 && i == 5) {
+        if (f6 && i == 5 && P.fext_world) {
+          // a world-frame wrench acts on link 6 as it is (GPU: i7m_linearize.h, FW)
+          for (int r = 0; r < 6; ++r) F0[i][r] = F0[i][r] - R(f6[r]);
+        } else if (f6 && i == 5) {
           R fw[3], nw[3];
           for (int r = 0; r < 3; ++r) {
             fw[r] = Rj[3 * r] * R(f6[0]) + Rj[3 * r + 1] * R(f6[1]) + Rj[3 * r + 2] * R(f6[2]);
@@ -558,6 +595,14 @@ struct Solver {
             dq[r] = dot6(S[r], y[j]);
             dv[r] = dot6(S[r], z[j]);
           }
+        }
+        if (f6 && P.fext_world) {
+          // the formulas above differentiate forces that turn with the bodies; a world-frame
+          // wrench does not, so d tau_r / d q_j gains +S_r . (S_j x* f_w) (i7m_linearize.h)
+          R fw6[6], tS[6];
+          for (int r = 0; r < 6; ++r) fw6[r] = R(f6[r]);
+          fcross(S[j], fw6, tS);
+          for (int r = 0; r < 6; ++r) dq[r] = dq[r] + dot6(S[r], tS);
         }
         chol6_solve(Lm, dq);
         chol6_solve(Lm, dv);
@@ -876,7 +921,13 @@ struct Solver {
         for (int i = 0; i < 6; ++i) uu = uu + x[12 + i] * x[12 + i];
         uc = uc + R(P.R) * uu;
         R L[6][6], a[6];
-        forward_dynamics(Md, c, s, x + 6, x + 12, f6, L, a);
+        double fl[6];
+        const double* fk = f6;
+        if (f6 && P.fext_world) {
+          wrench_world_to_local(Md, c, s, f6, fl);
+          fk = fl;
+        }
+        forward_dynamics(Md, c, s, x + 6, x + 12, fk, L, a);
         const R* xn = Xn + 18 * (k + 1);
         R eq = R(0), ev = R(0);
         for (int i = 0; i < 6; ++i) {
@@ -1308,12 +1359,24 @@ struct Solver {
       }
     }
     admm_it = it > A_.max_iter ? A_.max_iter : it;
+    if (!admm_solved) {
+      // OSQP after max_iter (oracle/osqp_admm.py OSQP.solve :344-349): the test at the final
+      // iterate unless the last iteration ran it, then the approximate one (eps x 10) -> 2
+      admm_Ax(x, Ax.data());
+      admm_Px(x, Px.data());
+      admm_Aty(y, Aty.data());
+      if (!checked && admm_converged(x, z, y, Ax.data(), Px.data(), Aty.data()))
+        admm_solved = 1;
+      else if (admm_converged(x, z, y, Ax.data(), Px.data(), Aty.data(), 10.0))
+        admm_solved = 2;
+    }
     *st.rho = rho;
     for (int e = 0; e < T; ++e) sol[e] = R(aD[e] * x[e]);
   }
   // OSQP's check_termination on the unscaled residuals, with OSQP 1.x's duality-gap test
   bool admm_converged(const double* x, const double* z, const double* y, const double* Ax, const double* Px,
-                      const double* Aty) const {
+                      const double* Aty, double es = 1.0) const {
+    const double ea = es * A_.eps_abs, er = es * A_.eps_rel;
     const int m = 12 * P.N;
     const double cinv = 1.0 / ac;
     double pr = 0.0, zn = 0.0, an = 0.0;
@@ -1334,14 +1397,14 @@ struct Solver {
       qx += aqs[e] * x[e];
     }
     dr *= cinv;
-    if (!(pr < A_.eps_abs + A_.eps_rel * std::max(zn, an))) return false;
-    if (!(dr < A_.eps_abs + A_.eps_rel * cinv * std::max(qn, std::max(atn, pxn)))) return false;
+    if (!(pr < ea + er * std::max(zn, an))) return false;
+    if (!(dr < ea + er * cinv * std::max(qn, std::max(atn, pxn)))) return false;
     if (A_.gap) {
       double sc = 0.0;
       for (int r = 0; r < m; ++r) sc += als[r] * std::max(y[r], 0.0) + als[r] * std::min(y[r], 0.0);
       xPx *= cinv; qx *= cinv; sc *= cinv;
       const double gap = xPx + qx + sc;
-      if (!(std::fabs(gap) < A_.eps_abs + A_.eps_rel * std::max(std::fabs(xPx), std::max(std::fabs(qx), std::fabs(sc)))))
+      if (!(std::fabs(gap) < ea + er * std::max(std::fabs(xPx), std::max(std::fabs(qx), std::fabs(sc)))))
         return false;
     }
     return true;
@@ -1351,7 +1414,8 @@ struct Solver {
   // box mode: ipm_it[qp] = the interior point's iterations of SQP iteration qp (may be null)
   // ADMM mode (st non-null): admm_it[qp] = OSQP iterations of SQP iteration qp
   int sqp(R* X, const R* xs, const double* goal, const double* f6, double* alphas, double* steps, int* n_alpha,
-          int* n_step, int* ipm_it = nullptr, AdmmState* st = nullptr, int* admm_its = nullptr) {
+          int* n_step, int* ipm_it = nullptr, AdmmState* st = nullptr, int* admm_its = nullptr,
+          int* admm_st = nullptr) {
     static const double AL[8] = {1.0, 0.5, 0.25, 0.125, 0.0625, 0.03125, 0.015625, 0.0078125};
     std::vector<R> Xn(T);
     *n_alpha = *n_step = 0;
@@ -1361,6 +1425,7 @@ struct Solver {
       if (st) {
         admm(X, xs, *st);
         if (admm_its) admm_its[qp] = admm_it;
+        if (admm_st) admm_st[qp] = admm_solved;
       } else {
         riccati(X, xs);
       }
@@ -1394,12 +1459,13 @@ struct Solver {
 };
 
 Params make_params(int N, const double* cfg, int goal_stride) {
-  // cfg: dt, dQ, R, QN, eps, mu, step_tol, regularize, max_iters
+  // cfg: dt, dQ, R, QN, eps, mu, step_tol, regularize, max_iters, fext_world
   Params P;
   P.N = N;
   P.dt = cfg[0]; P.dQ = cfg[1]; P.R = cfg[2]; P.QN = cfg[3]; P.eps = cfg[4]; P.mu = cfg[5]; P.step_tol = cfg[6];
   P.regularize = (int)cfg[7];
   P.max_iters = (int)cfg[8];
+  P.fext_world = (int)cfg[9];
   P.goal_stride = goal_stride;
   P.box_mask = 0;
   P.box_max_iters = 30;
@@ -1450,12 +1516,13 @@ int i7m_cpu_solve_box(const double* model_packed, int N, const double* cfg, cons
 // adaptive_rho_tolerance.  The solver state of every problem (scaled x (B, T), z (B, 12N),
 // y (B, 12N), the previous QP's q (B, T), rho (B)) is read and written back: it is the
 // reference's OSQP object, warm-started from call to call (src/osqp_solver.py:38-40).
-// admm_iters (B, 8): OSQP iterations per SQP iteration (may be null).
+// admm_iters (B, 8): OSQP iterations per SQP iteration; admm_status (B, 8): 1 solved, 2 solved
+// inaccurate, 0 max_iter reached (as i7m_get_admm_status); either may be null.
 int i7m_cpu_solve_admm(const double* model_packed, int N, const double* cfg, const double* admm_cfg, int B,
                        const double* xu_in, const double* xcur, const double* goals, int goal_stride,
                        const double* fext, double* xu_out, int* qp_iters, double* alphas, double* steps,
                        double* st_x, double* st_z, double* st_y, double* st_q, double* st_rho, int* admm_iters,
-                       int nthreads) {
+                       int* admm_status, int nthreads) {
   if (N < 2 || N > 64 || B < 0 || !admm_cfg) return -1;
   const Model M = make_model(model_packed);
   Params P = make_params(N, cfg, goal_stride);
@@ -1476,7 +1543,8 @@ int i7m_cpu_solve_admm(const double* model_packed, int N, const double* cfg, con
     int na, ns;
     qp_iters[b] = S.sqp(X, xcur + 12 * (size_t)b, goals + (size_t)b * N * goal_stride, fext ? fext + 6 * (size_t)b : nullptr,
                         alphas + 8 * (size_t)b, steps + 8 * (size_t)b, &na, &ns, nullptr, &st,
-                        admm_iters ? admm_iters + 8 * (size_t)b : nullptr);
+                        admm_iters ? admm_iters + 8 * (size_t)b : nullptr,
+                        admm_status ? admm_status + 8 * (size_t)b : nullptr);
   }
   return 0;
 }

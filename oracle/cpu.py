@@ -29,7 +29,7 @@ def load(path=None):
                                            _DP, _DP, _IP, _IP, _DP, C.c_int]
         _lib.i7m_cpu_count_flops_box.argtypes = [_DP, C.c_int, _DP, _DP, _DP, _DP, _DP, C.c_int, _DP]
         _lib.i7m_cpu_solve_admm.argtypes = [_DP, C.c_int, _DP, _DP, C.c_int, _DP, _DP, _DP, C.c_int, _DP, _DP, _IP,
-                                            _DP, _DP, _DP, _DP, _DP, _DP, _DP, _IP, C.c_int]
+                                            _DP, _DP, _DP, _DP, _DP, _DP, _DP, _IP, _IP, C.c_int]
     return _lib
 
 
@@ -37,8 +37,15 @@ def _p(a):
     return a.ctypes.data_as(_DP)
 
 
-def _cfg(dt=0.01, dQ=0.01, R=1e-5, QN=100.0, eps=1.0, mu=10.0, step_tol=1e-3, regularize=True, max_iters=2):
-    return np.array([dt, dQ, R, QN, eps, mu, step_tol, float(regularize), float(max_iters)])
+def _cfg(dt=0.01, dQ=0.01, R=1e-5, QN=100.0, eps=1.0, mu=10.0, step_tol=1e-3, regularize=True, max_iters=2,
+         fext_frame="local"):
+    """fext_frame: "local" = the wrench is constant in joint 6's frame (pinocchio f_ext); "world" =
+    a world-frame spatial force about the world origin, converted per configuration by
+    oMi[6].actInv like the GPU's I7M_WRENCH_WORLD (batch_sqp's default)."""
+    if fext_frame not in ("local", "world"):
+        raise ValueError("fext_frame must be 'local' or 'world'")
+    return np.array([dt, dQ, R, QN, eps, mu, step_tol, float(regularize), float(max_iters),
+                     float(fext_frame == "world")])
 
 
 def model_packed():
@@ -114,11 +121,15 @@ class AdmmState:
         self.y = np.zeros((B, m))
         self.q = np.zeros((B, T))
         self.rho = np.full(B, float(rho))
+        # OSQP's status of every SQP iteration's QP in the last solve_admm (B, 8): 1 solved,
+        # 2 solved inaccurate, 0 max_iter reached, -1 no QP (i7m_get_admm_status's codes)
+        self.status = np.full((B, 8), -1, dtype=np.int32)
 
 
 def solve_admm(xcur, goals, XU, N, state, nthreads=1, fext=None, admm=None, **cfg):
     """ADMM mode: (XU out, qp_iters, alphas, steps, OSQP iterations (B, 8) per SQP iteration);
-    `state` (AdmmState) is updated in place."""
+    `state` (AdmmState) is updated in place.  fext (B, 6) with cfg fext_frame "local" (default) or
+    "world" (batch_sqp's default, gato_controller.py's hypotheses)."""
     lib = load()
     XU = np.ascontiguousarray(XU, float)
     B = XU.shape[0]
@@ -136,10 +147,11 @@ def solve_admm(xcur, goals, XU, N, state, nthreads=1, fext=None, admm=None, **cf
     ac = admm_cfg() if admm is None else np.asarray(admm, float)
     for a in (state.x, state.z, state.y, state.q, state.rho):
         assert a.flags.c_contiguous and a.dtype == np.float64 and a.shape[0] == B
+    state.status[:] = -1
     rc = lib.i7m_cpu_solve_admm(_p(m), N, _p(c), _p(ac), B, _p(XU), _p(xcur), _p(goals), stride,
                                 _p(f) if f is not None else None, _p(out), qp.ctypes.data_as(_IP), _p(al), _p(st),
                                 _p(state.x), _p(state.z), _p(state.y), _p(state.q), _p(state.rho),
-                                it.ctypes.data_as(_IP), int(nthreads))
+                                it.ctypes.data_as(_IP), state.status.ctypes.data_as(_IP), int(nthreads))
     if rc != 0:
         raise RuntimeError("i7m_cpu_solve_admm failed")
     return out, qp, al, st, it

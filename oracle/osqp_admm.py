@@ -130,7 +130,7 @@ class OSQP:
         self.y = np.zeros(self.m)
         self._lu = None
         self.info = {}
-        self.history = []  # per solve: (iters, rho at exit, rho updates)
+        self.history = []  # per solve: (iters, rho at exit, rho updates, checks, rho estimates, status)
 
     # ---- scaling (OSQP scaling.c) ----
     def _scale_data(self):
@@ -350,7 +350,7 @@ class OSQP:
         self.x, self.z, self.y = x, z, y
         self.info = dict(iter=it, status=status, pri_res=f["pri_res"], dua_res=f["dua_res"],
                          rho=self.rho, rho_updates=rho_updates)
-        self.history.append((it, self.rho, rho_updates, list(self.checks), list(self.rho_estimates)))
+        self.history.append((it, self.rho, rho_updates, list(self.checks), list(self.rho_estimates), status))
         if status in ("primal_infeasible", "dual_infeasible", "non_convex"):
             self.x[:], self.z[:], self.y[:] = 0.0, 0.0, 0.0
             return np.full(n, np.nan), np.full(self.m, np.nan)

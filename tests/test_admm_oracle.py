@@ -164,3 +164,91 @@ def test_direct_mode_vs_osqp_distribution_is_pinned():
     assert 3e-5 < np.median(rel) < 1.2e-4, np.median(rel)
     assert 0.2 < (rel > 1e-4).mean() < 0.45, (rel > 1e-4).mean()
     assert rel.max() < 1e-2, rel.max()
+
+
+def _world_forces(B, seed):
+    """World-frame wrench hypotheses as gato_controller.py:77-81,120-129 draws them: forces only
+    (torque part zero), row 0 zero."""
+    f = np.random.default_rng(seed).normal(0, 30, (B, 6))
+    f[:, 3:] = 0.0
+    f[0] = 0.0
+    return f
+
+
+def test_port_world_wrench_direct_matches_numpy_oracle():
+    """The port's world-frame wrench (cfg fext_frame "world": F0 -= f_w in the linearisation with
+    the +S_r.(S_j x* f_w) term a world-fixed force adds to d tau / dq, actInv per configuration in
+    the merit) against the numpy oracle, whose derivatives are complex-step through rbd.fext_list:
+    alpha sequences identical, XU 1e-8 (exact QP both sides)."""
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, 13)
+    f = _world_forces(B, 1)
+    f[3, 3:] = [0.5, -0.5, 1.0]
+    out, qp, al, _ = cpu.solve(xcur, goals, XU, N, fext=f, fext_frame="world")
+    loc, *_ = cpu.solve(xcur, goals, XU, N, fext=f, fext_frame="local")
+    for b in range(B):
+        sq = SQPRef(OSQPSolverRef(N=N, fext6=f[b], fext_frame="world"))
+        x = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        np.testing.assert_array_equal(sq.stats["linesearch_alphas"]["values"], al[b, :qp[b]])
+        assert np.linalg.norm(x - out[b]) <= 1e-8 * np.linalg.norm(x), b
+        if b:
+            assert not np.allclose(out[b], loc[b])  # the frames are different models
+
+
+def test_port_admm_world_wrench_matches_numpy_osqp():
+    """batch_sqp's default (ADMM mode, world-frame wrench, gato_controller.py:90,95,129-138) on the
+    port against the numpy OSQP restatement with the same wrench: two consecutive solves with
+    resetLambda (OSQP's y = 0) between them; OSQP iterations and alphas identical, XU 1e-8."""
+    N, B = 16, 4
+    xcur, goals, XU = synthetic_batch(B, N, 17)
+    f = _world_forces(B, 3)
+    st = cpu.AdmmState(B, N)
+    out, qp, al, _, it = cpu.solve_admm(xcur, goals, XU, N, st, fext=f, fext_frame="world")
+    st.y[:] = 0.0  # resetLambda
+    out2, qp2, al2, _, it2 = cpu.solve_admm(xcur, goals, out, N, st, fext=f, fext_frame="world")
+    for b in range(B):
+        s = OSQPSolverRef(N=N, qp="osqp", fext6=f[b], fext_frame="world")
+        sq = SQPRef(s)
+        x = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        its = [h[0] for h in s.osqp.history]
+        assert its == list(it[b, :qp[b]]), (b, its, it[b])
+        np.testing.assert_array_equal(sq.stats["linesearch_alphas"]["values"], al[b, :qp[b]])
+        assert np.linalg.norm(x - out[b]) <= 1e-8 * np.linalg.norm(x), b
+        s.osqp.y[:] = 0.0
+        n0 = len(sq.stats["linesearch_alphas"]["values"])
+        x2 = sq.sqp(xcur[b], goals[b], x.copy())
+        assert [h[0] for h in s.osqp.history][len(its):] == list(it2[b, :qp2[b]]), b
+        np.testing.assert_array_equal(sq.stats["linesearch_alphas"]["values"][n0:], al2[b, :qp2[b]])
+        assert np.linalg.norm(x2 - out2[b]) <= 1e-8 * np.linalg.norm(x2), b
+
+
+STATUS_CODE = {"solved": 1, "solved_inaccurate": 2, "max_iter_reached": 0}
+
+
+@pytest.mark.parametrize("max_iter,eps", [(10, 1e-3), (20, 1e-3), (50, 1e-8)])
+def test_port_admm_status_after_max_iter_matches_numpy_osqp(max_iter, eps):
+    """OSQP's status when max_iter stops the iteration: the test once more at the final
+    iterate unless the last iteration ran it, then the approximate test (eps x 10, "solved
+    inaccurate").  max_iter 10 / 20: the closing exact test runs (no multiple of 25); 50 (eps
+    1e-8): only the approximate one.  Port status per QP (i7m_get_admm_status's codes) = the numpy
+    restatement's, OSQP iterations and alphas identical."""
+    N, B = 16, 8
+    xcur, goals, XU = synthetic_batch(B, N, 41)
+    st = cpu.AdmmState(B, N)
+    cfg = dict(max_iter=max_iter, eps_abs=eps, eps_rel=eps)
+    out, qp, al, _, it = cpu.solve_admm(xcur, goals, XU, N, st, admm=cpu.admm_cfg(**cfg))
+    seen = set()
+    for b in range(B):
+        s = OSQPSolverRef(N=N, qp="osqp", osqp_settings=cfg)
+        sq = SQPRef(s)
+        x = sq.sqp(xcur[b], goals[b], XU[b].copy())
+        assert [h[0] for h in s.osqp.history] == list(it[b, :qp[b]]), b
+        codes = [STATUS_CODE[h[5]] for h in s.osqp.history]
+        assert codes == list(st.status[b, :qp[b]]), (b, codes, st.status[b])
+        assert (st.status[b, qp[b]:] == -1).all()
+        np.testing.assert_array_equal(sq.stats["linesearch_alphas"]["values"], al[b, :qp[b]])
+        assert np.linalg.norm(x - out[b]) <= 1e-8 * np.linalg.norm(x), b
+        seen.update(codes)
+    # the cases each setting is for: no test can pass / inaccurate after the closing tests /
+    # inaccurate after the approximate test alone
+    assert {10: {0}, 20: {0, 2}, 50: {1, 2}}[max_iter] <= seen, seen

@@ -335,3 +335,36 @@ def test_admm_state_over_2gib_is_refused(lib, model):
     with pytest.raises(Exception, match="2 GiB"):
         lib.Handle(model, N=64, max_batch=200000, qp_mode=lib.QP_ADMM)
 
+
+
+@pytest.mark.parametrize("max_iter,eps", [(20, 1e-3), (50, 1e-8)])
+def test_admm_status_after_max_iter_matches_port(lib, model, max_iter, eps):
+    """OSQP's closing tests after max_iter (oracle/osqp_admm.py OSQP.solve :344-349):
+    k_admm_iter runs the termination test at the final iterate unless the last iteration ran it, then
+    the approximate test (eps x 10) -> status 2 "solved inaccurate".  (20, 1e-3): 20 is no multiple
+    of check_termination 25, so both closing tests run — statuses 0, 1 and 2 all occur; (50, 1e-8):
+    only the approximate one.  Status, OSQP iterations, alphas = the port's (itself = the numpy
+    restatement's, tests/test_admm_oracle.py::test_port_admm_status_after_max_iter_matches_numpy_osqp);
+    QPSolution maps the codes to OSQP's strings."""
+    from indy7_mpc_amd.osqp_solver import QPSolution
+    N, B = 16, 64
+    cfg = dict(max_iter=max_iter, eps_abs=eps, eps_rel=eps)
+    xcur, goals, XU = synthetic_batch(B, N, 41)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, admm=cfg)
+    out, s = h.solve(xcur, goals, XU)
+    it, _, stat = h.admm_stats(B, with_status=True)
+    st = cpu.AdmmState(B, N)
+    ref, qp, al, _, it_r = cpu.solve_admm(xcur, goals, XU, N, st, admm=cpu.admm_cfg(**cfg))
+    np.testing.assert_array_equal(s["qp_iters"], qp)
+    ran = np.arange(8)[None, :] < qp[:, None]
+    np.testing.assert_array_equal(np.where(ran, it, -1), np.where(ran, it_r, -1))
+    np.testing.assert_array_equal(np.where(ran, stat, -9), np.where(ran, st.status, -9))
+    assert (stat[~ran] == -1).all()
+    seen = set(stat[ran].tolist())
+    assert ({0, 1, 2} if max_iter == 20 else {1, 2}) <= seen, seen
+    assert _rel(out, ref).max() < 5e-8
+    assert [QPSolution.from_admm(None, c, 1, None).info.status for c in (1, 2, 0)] == \
+        ["solved", "solved inaccurate", "maximum iterations reached"]
+    assert [QPSolution.from_admm(None, c, 1, None).info.status_val for c in (1, 2, 0)] == [1, 2, -2]
+    with pytest.raises(RuntimeError, match="no OSQP result"):
+        QPSolution.from_admm(None, -1, 0, None)

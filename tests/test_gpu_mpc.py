@@ -173,3 +173,76 @@ def test_mpc_run_refuses_a_handle_with_a_wrench(lib, model):
     h.set_external_wrench(None)
     d, _, _, _ = h.mpc_run(xs, ends, 2)
     assert np.isfinite(d).all()
+
+
+def test_closed_loop_500_steps_admm_default_shadowed_by_port(lib, model):
+    """The drop-in default (OSQPSolver(model): qp_mode "admm", OSQP's iteration with its carried
+    state) through the notebook's whole 500-step closed loop (pin_mpc_indy7.ipynb:98-597,
+    src/osqp_mpc.py:14-72), shadowed at EVERY one of the 501 SQP calls: the GPU's carried OSQP
+    state (scaled x, z, y, the previous q, rho) is read before the call, and the C++ port's ADMM
+    mode (pinned to the numpy OSQP restatement, tests/test_admm_oracle.py) re-solves the recorded
+    (xcur, goal, XU) from that same state.  OSQP iterations per QP, alphas and SQP iteration counts
+    identical, the next XU to 1e-8 relative, OSQP's status of every QP; every rk4 plant step from
+    the GPU's state and control to 1e-12.  (The warm start carries x, z, y, q and rho from call to
+    call: the long horizon is where a drift in the carried state would show.)"""
+    from indy7_mpc_amd.osqp_mpc import MPC_OSQP
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+    from oracle import cpu
+
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    solver = OSQPSolver(model)
+    assert solver.box["qp_mode"] == lib.QP_ADMM
+    h = solver.handle
+    sqp = SQP_OSQP(solver)
+    rec = []
+    inner = sqp.sqp
+
+    def recording_sqp(xcur, goals, XU):
+        x_in, g_in, xu_in = (np.array(a, dtype=float) for a in (xcur, goals, XU))
+        state = [a[0].copy() for a in h.admm_state(1)]  # x, z, y, q (rows) and rho (scalar)
+        n0 = len(sqp.stats["linesearch_alphas"]["values"])
+        out = inner(xcur, goals, XU)
+        its, _, stat = h.admm_stats(1, with_status=True)
+        rec.append((x_in, g_in, xu_in, np.array(out), list(sqp.stats["linesearch_alphas"]["values"][n0:]),
+                    sqp.stats["qp_iters"]["values"][-1], state, its[0].copy(), stat[0].copy()))
+        return out
+
+    sqp.sqp = recording_sqp
+    ctrl = MPC_OSQP(model, sqp, solver)
+    ends = np.array([solver.eepos(np.array(q)) for q in tr["endpoint_q"]])
+    ctrl.run_mpc(np.array(tr["xstart"]), ends, num_steps=500, verbose=False)
+    assert len(rec) == 501 and len(ctrl.xpath) == 500
+
+    n = len(rec)
+    xs = np.stack([r[0] for r in rec])
+    gs = np.stack([r[1] for r in rec])
+    xus = np.stack([r[2] for r in rec])
+    outs = np.stack([r[3] for r in rec])
+    st = cpu.AdmmState(n, 32)
+    for i, r in enumerate(rec):
+        st.x[i], st.z[i], st.y[i], st.q[i], st.rho[i] = r[6]
+    assert not st.y[0].any() and st.y[1:].any()  # a fresh solver, then the carried duals
+    ref, qp, al, _, it = cpu.solve_admm(xs, gs, xus, 32, st, nthreads=min(16, os.cpu_count() or 1))
+    rel = np.linalg.norm(outs - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert rel.max() < 1e-8, (int(rel.argmax()), rel.max(), np.median(rel))
+    for i, r in enumerate(rec):
+        assert r[5] == qp[i], i
+        np.testing.assert_array_equal(np.array(r[4]), al[i][~np.isnan(al[i])], err_msg=f"step {i}")
+        np.testing.assert_array_equal(r[7][:qp[i]], it[i, :qp[i]], err_msg=f"step {i}")
+        np.testing.assert_array_equal(r[8][:qp[i]], st.status[i, :qp[i]], err_msg=f"step {i}")
+    assert (it[:, 0] % 25 == 0).all() and (st.status[:, 0] == 1).all()
+    # the carried state after a call is the next call's input state: the port's state after
+    # re-solving record i equals the GPU's state read before record i + 1
+    for i in range(0, n - 1, 50):
+        nxt = rec[i + 1][6]
+        for a, b_ in ((st.x[i], nxt[0]), (st.z[i], nxt[1]), (st.y[i], nxt[2]), (st.q[i], nxt[3])):
+            assert np.linalg.norm(a - b_) <= 1e-7 * max(np.linalg.norm(b_), 1e-300), i
+        assert st.rho[i] == nxt[4]
+    for i in range(500):
+        x, u = xs[i + 1], xus[i + 1][12:18]
+        qn, vn = rbd.rk4(x[:6], x[6:], u, 0.01)
+        nxt = np.concatenate([qn, vn])
+        got = xs[i + 2] if i < 499 else np.concatenate([ctrl.xpath[-1], np.full(6, np.nan)])
+        k = 12 if i < 499 else 6
+        assert np.linalg.norm(nxt[:k] - got[:k]) <= 1e-12 * np.linalg.norm(nxt[:k]), i

@@ -5,7 +5,10 @@ gfx950 FETCH_SIZE reads 1/2 of a wide coalesced read -> x2).
 
     python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --batch 4096 --N 32 [--out profiles/pmc_traffic.json]
 Launches of the timed batch size only (grid size identifies them); median over launches of the
-first SQP iteration (all problems active) is reported.
+first SQP iteration (all problems active) is reported.  --admm-stagger: k_admm_iter's launches of
+ADMM mode's two staggered ranges (batch / 2 problems each, both SQP iterations), MEAN over every
+such launch — the per-launch average bench.py's event pass reports beside it — under the key
+k_admm_iter:B<batch/2>:N<N>:stagger.
 """
 import argparse
 import collections
@@ -46,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json"))
+    ap.add_argument("--admm-stagger", action="store_true")
     a = ap.parse_args()
     f = per_kernel(a.fetch, "FETCH_SIZE")
     w = per_kernel(a.write, "WRITE_SIZE")
@@ -69,6 +73,19 @@ def main():
         d[f"{k}:B{a.batch}:N{a.N}"] = {"hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_corrected": fetch_b,
                                        "write_bytes": write_b, "fetch_kib_raw_median": statistics.median(f1),
                                        "launches": len(fv)}
+    if a.admm_stagger:
+        hb = a.batch // 2
+        g = -(-hb // 4) * 64
+        gg = [key for key in f if key[0] == "k_admm_iter" and key[1] == g]
+        if gg:
+            fv, wv = f[gg[0]], w.get(gg[0], [0.0])
+            fetch_b = 2.0 * 1024.0 * statistics.mean(fv)
+            write_b = 1024.0 * statistics.mean(wv)
+            d[f"k_admm_iter:B{hb}:N{a.N}:stagger"] = {
+                "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
+                "fetch_kib_raw_mean": statistics.mean(fv), "launches": len(fv),
+                "fetch_kib_raw_per_launch": fv, "write_kib_per_launch": wv,
+                "note": "mean over every launch of the staggered ranges (both SQP iterations)"}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(d, open(a.out, "w"), indent=1)
     print(json.dumps(d, indent=1))
