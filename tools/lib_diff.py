@@ -37,6 +37,20 @@ def dump(path):
     ends = h.eepos(np.array(tr["endpoint_q"]))
     out["mpc"] = h.mpc_run(np.array([tr["xstart"]]), ends, 500)[0][:, 0]
     h.close()
+    # ADMM mode (the drop-in default): config 3 twice (cold, then warm from the carried state), the
+    # carried state after it, N = 64 and an odd batch (empty rows of the 3- and 4-problem waves)
+    for key, (B, N, seed) in {"a3": (4096, 32, 45), "a64": (24, 64, 48), "a13": (13, 32, 50)}.items():
+        xc, g, xu = synthetic_batch(B, N, seed)
+        h = _lib.Handle(m, N=N, max_batch=B, qp_mode=_lib.QP_ADMM)
+        o1 = h.solve(xc, g, xu)[0]
+        o2 = h.solve(xc, g, o1)[0]
+        out[key] = np.concatenate([o1, o2], axis=1)
+        out[key + "_state"] = np.concatenate(h.admm_state(B)[:4], axis=1)
+        out[key + "_iters"] = h.admm_stats(B)[0]
+        h.close()
+    h = _lib.Handle(m, N=32, max_batch=1, qp_mode=_lib.QP_ADMM)
+    out["mpca"] = h.mpc_run(np.array([tr["xstart"]]), ends, 40)[0][:, 0]
+    h.close()
     out["ver"] = np.array(_lib.version())
     np.savez(path, **out)
 
@@ -44,14 +58,19 @@ def dump(path):
 def cmp(a, b):
     A, B = np.load(a), np.load(b)
     print("A:", str(A["ver"]), "\nB:", str(B["ver"]))
-    for k in ("c3", "c4"):
-        x, y = A[k], B[k]
+    for k in ("c3", "c4", "a3", "a3_state", "a3_iters", "a64", "a64_state", "a13", "a13_state"):
+        if k not in A or k not in B:
+            continue
+        x, y = A[k].astype(float), B[k].astype(float)
         diff = (x != y).any(axis=1)
         rel = np.linalg.norm(x - y, axis=1) / np.maximum(np.linalg.norm(x, axis=1), 1e-300)
         print(f"{k}: {int(diff.sum())} of {len(x)} problems differ; max rel {rel.max():.2e}")
-    x, y = A["mpc"], B["mpc"]
-    nz = np.nonzero(x != y)[0]
-    print(f"mpc: first differing step {nz[0] if len(nz) else None}; max |diff| {np.abs(x - y).max():.3e}")
+    for k in ("mpc", "mpca"):
+        if k not in A or k not in B:
+            continue
+        x, y = A[k], B[k]
+        nz = np.nonzero((x != y) & ~(np.isnan(x) & np.isnan(y)))[0]
+        print(f"{k}: first differing step {nz[0] if len(nz) else None}; max |diff| {np.nanmax(np.abs(x - y)):.3e}")
 
 
 if __name__ == "__main__":
