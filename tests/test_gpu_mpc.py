@@ -182,9 +182,12 @@ def test_closed_loop_500_steps_admm_default_shadowed_by_port(lib, model):
     state (scaled x, z, y, the previous q, rho) is read before the call, and the C++ port's ADMM
     mode (pinned to the numpy OSQP restatement, tests/test_admm_oracle.py) re-solves the recorded
     (xcur, goal, XU) from that same state.  OSQP iterations per QP, alphas and SQP iteration counts
-    identical, the next XU to 1e-8 relative, OSQP's status of every QP; every rk4 plant step from
-    the GPU's state and control to 1e-12.  (The warm start carries x, z, y, q and rho from call to
-    call: the long horizon is where a drift in the carried state would show.)"""
+    identical, OSQP's status of every QP, the next XU to 5e-8 relative (tests/test_gpu_admm.py's ADMM
+    tolerance: the x-update's summation order differs between the port and the device, and a QP of
+    cond ~4e7 amplifies that rounding; measured over the 501 calls: median 1.6e-9, max 3.6e-8 at call
+    96); every rk4 plant step from the GPU's state and control to 1e-12.  (The warm start carries x,
+    z, y, q and rho from call to call: the long horizon is where a drift in the carried state would
+    show.)"""
     from indy7_mpc_amd.osqp_mpc import MPC_OSQP
     from indy7_mpc_amd.osqp_solver import OSQPSolver
     from indy7_mpc_amd.osqp_sqp import SQP_OSQP
@@ -225,7 +228,7 @@ def test_closed_loop_500_steps_admm_default_shadowed_by_port(lib, model):
     assert not st.y[0].any() and st.y[1:].any()  # a fresh solver, then the carried duals
     ref, qp, al, _, it = cpu.solve_admm(xs, gs, xus, 32, st, nthreads=min(16, os.cpu_count() or 1))
     rel = np.linalg.norm(outs - ref, axis=1) / np.linalg.norm(ref, axis=1)
-    assert rel.max() < 1e-8, (int(rel.argmax()), rel.max(), np.median(rel))
+    assert rel.max() < 5e-8 and np.median(rel) < 5e-9, (int(rel.argmax()), rel.max(), np.median(rel))
     for i, r in enumerate(rec):
         assert r[5] == qp[i], i
         np.testing.assert_array_equal(np.array(r[4]), al[i][~np.isnan(al[i])], err_msg=f"step {i}")
