@@ -73,7 +73,10 @@ struct AdmmArgs {
 #define I7M_ADMM_FSTRIDE 19  // the register factor's LDS row stride for S and C (18: 3-way bank conflicts on row reads)
 #endif
 #ifndef I7M_ADMM_FACTOR
-#define I7M_ADMM_FACTOR 2  // 3: three problems per wave (adm_factor3), 2: register Cholesky at one (adm_factor), 1: LDS-staged (adm_factor_lds)
+#define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
+#endif
+#ifndef I7M_ADMM_CHOL_OVERLAP
+#define I7M_ADMM_CHOL_OVERLAP 1  // the factor's pivot column to LDS unscaled, under the pivot's sqrt / reciprocal
 #endif
 #ifndef I7M_ADMM_SCALE_WPE
 #define I7M_ADMM_SCALE_WPE 2  // (N <= 32: the linearisation magnitudes stay in registers for all ten passes)
@@ -677,17 +680,30 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     double myid = 1.0;  // 1 / L_ll of this lane's row (the inverse multiplies by it)
 #pragma unroll
     for (int p = 0; p < 18; ++p) {
+#if I7M_ADMM_CHOL_OVERLAP
+      // column p goes to LDS UNSCALED, before the pivot's square root and reciprocal, so its round
+      // trip runs under them; a reader scales the entry itself (col[j] * id is the product the
+      // writing lane formed before, the same two operands: bit-identical)
+      double* col = sCol + 32 * (p & 1);
+      if (p < 17 && l < 18) col[l] = r[p];
+#endif
       const double d = sqrt(adm_readlane(r[p], p));
       const double id = 1.0 / d;
       myid = l == p ? id : myid;
       r[p] = l == p ? d : (l > p ? r[p] * id : r[p]);
       if (p < 17) {
+#if I7M_ADMM_CHOL_OVERLAP
+        wave_sync();
+#pragma unroll
+        for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * (col[j] * id);
+#else
         // column p of L to the wave through LDS (double-buffered: no wait for the last reads)
         double* col = sCol + 32 * (p & 1);
         if (l < 18) col[l] = r[p];
         wave_sync();
 #pragma unroll
         for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
+#endif
       }
     }
     wave_sync();  // every lane has read S before L overwrites it
@@ -1464,207 +1480,6 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   }
 }
 
-// k_admm_factor at three problems per wave (I7M_ADMM_FACTOR 3, the default): lanes 21 g .. 21 g + 20
-// work on problem g of the wave (lane 63 shadows group 2); the Cholesky and the inverse run with
-// row / column i in lane 21 g + i of every group at once (18 of 64 lanes busy at one problem per
-// wave: the same instruction stream now serves three), the element passes (J staged dense, S's
-// lower triangle, C_k) spread the three problems' entries over all 64 lanes.  Per problem exactly
-// adm_factor's operations in its order, so the records are bit-identical.  A stage's operands
-// (three problems x 198 doubles) arrive one stage ahead by five LDS-DMA wave-instructions.
-// LDS per wave 38.4 KB (four waves per CU): the launch is one wave per SIMD.
-constexpr int AF3_G = 3, AF3_W = 21;            // problems per wave, lanes per problem
-constexpr int AF3_PC = 198;                     // stage operands per problem (doubles): J 120 | Pq 36 | Pd 18 | I_k 12 | I_{k+1} 12
-constexpr int AF3_STG = 640;                    // one stage buffer: 5 wave-instructions x 64 lanes x 16 B
-constexpr int AF3_NI = 5;                       // DMA wave-instructions per stage (320 >= 3 x 99 pieces)
-struct AdmF3Lds {
-  double stg[2 * AF3_STG];
-  double S[AF3_G][18 * I7M_ADMM_FSTRIDE];
-  double J[AF3_G][216];
-  double L[AF3_G][324];
-  double Cp[AF3_G][12 * I7M_ADMM_FSTRIDE];
-  double col[AF3_G][64];
-};
-__device__ __forceinline__ void adm_factor3(const AdmmArgs& a, AdmF3Lds& sm) {
-  const SolveParams& P = a.P;
-  const int N = P.N, T = P.T, m = 12 * N;
-  const double sigma = a.A.sigma;
-  constexpr int FS = I7M_ADMM_FSTRIDE;
-  const int l = threadIdx.x;
-  const int gl = l / AF3_W < AF3_G ? l / AF3_W : AF3_G - 1;  // this lane's problem (lane 63: group 2)
-  const int li = l - AF3_W * gl, lr = li < 18 ? li : 17;
-  const int b0 = a.b0 + AF3_G * (int)blockIdx.x;
-  bool okq[AF3_G];
-  double req[AF3_G];
-#pragma unroll
-  for (int q = 0; q < AF3_G; ++q) {
-    const int b = b0 + q;
-    okq[q] = b < P.B && !(a.active && !a.active[b]);
-    req[q] = okq[q] ? 1e3 * a.srho[b] : 0.0;
-  }
-  if (!okq[0] && !okq[1] && !okq[2]) return;
-  const bool mine = okq[gl] && li < 18;  // this lane stores rows / columns of its problem
-  const double re = gl == 0 ? req[0] : (gl == 1 ? req[1] : req[2]);
-  const auto rA = a4_rsrc(a.abase, a.abytes);
-  auto boff = [&](const double* q) { return (unsigned)__builtin_amdgcn_readfirstlane((int)((const char*)q - (const char*)a.abase)); };
-  const unsigned oR = boff(a.R), oPq = boff(a.Pq), oPd = boff(a.Pd), oI = boff(a.I);
-  const unsigned stg_lds = (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)sm.stg;
-  // DMA piece g = 64 u + l: problem q = g / 99, its piece j = g % 99: [0, 60) J, [60, 78) Pq,
-  // [78, 87) Pd, [87, 99) I_k and I_{k+1}; stage k's source = base + k * step
-  unsigned vb[AF3_NI], vs[AF3_NI];
-#pragma unroll
-  for (int u = 0; u < AF3_NI; ++u) {
-    const int g = 64 * u + l, q = g / 99, j = g - 99 * q;
-    const int b = b0 + (q < AF3_G ? q : 0);
-    const bool ok = q < AF3_G && (q == 0 ? okq[0] : (q == 1 ? okq[1] : okq[2]));
-    unsigned o, st;
-    if (j < 60) {
-      o = oR + 8u * (unsigned)(b * N * ADM_REC + REC_J) + 16u * j;
-      st = 8u * ADM_REC;
-    } else if (j < 78) {
-      o = oPq + 8u * (unsigned)(b * N * 36) + 16u * (j - 60);
-      st = 8u * 36;
-    } else if (j < 87) {
-      o = oPd + 8u * (unsigned)(b * T) + 16u * (j - 78);
-      st = 8u * 18;
-    } else {
-      o = oI + 8u * (unsigned)(b * m) + 16u * (j - 87);
-      st = 8u * 12;
-    }
-    vb[u] = (ok ? o : A5_OOB) - 1024u * (unsigned)(u & 3);
-    vs[u] = ok ? st : 0u;
-  }
-  auto fetch = [&](int k) {
-    unsigned vo[AF3_NI];
-#pragma unroll
-    for (int u = 0; u < AF3_NI; ++u) vo[u] = vb[u] + (unsigned)k * vs[u];
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %7, 0 offen lds\n\t"
-        "buffer_load_dwordx4 %3, %7, 0 offen offset:1024 lds\n\t"
-        "buffer_load_dwordx4 %4, %7, 0 offen offset:2048 lds\n\t"
-        "buffer_load_dwordx4 %5, %7, 0 offen offset:3072 lds\n\t"
-        "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %6, %7, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(__builtin_amdgcn_readfirstlane(stg_lds + 8u * AF3_STG * (k & 1))), "v"(vo[0]), "v"(vo[1]), "v"(vo[2]),
-          "v"(vo[3]), "v"(vo[4]), "s"(rA)
-        : "memory");
-  };
-  // this lane's record stores: problem gl's record base (masked past the range when not `mine`)
-  const unsigned oRec = mine ? oR + 8u * (unsigned)((b0 + gl) * N * ADM_REC) : A5_OOB;
-  fetch(0);
-  for (int k = 0; k < N; ++k) {
-    const int nk = k < N - 1 ? 18 : 12;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage k's operands have landed
-    if (k + 1 < N) fetch(k + 1);
-    const double* Gs = sm.stg + AF3_STG * (k & 1);  // problem q's operands at Gs + AF3_PC q
-    if (k < N - 1) {
-      // J_k dense (12 x 18) per problem from its compact form
-      for (int e = l; e < AF3_G * 216; e += 64) {
-        const int q = e / 216, ee = e - 216 * q, i = ee / 18, j = ee - 18 * i;
-        const double* Jc = Gs + AF3_PC * q;
-        double v;
-        if (i < 6) v = j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
-        else v = Jc[12 + 18 * (i - 6) + j];
-        sm.J[q][ee] = v;
-      }
-    }
-    wave_sync();
-    // S's lower triangle, the three problems' 513 entries over the wave (adm_factor's formulas)
-#pragma unroll 1
-    for (int t = 0; t < 9; ++t) {
-      const int e = l + 64 * t;
-      if (e < AF3_G * 171) {
-        const int q = e / 171, ee = e - 171 * q;
-        int i = (int)((sqrtf(8.0f * (float)ee + 1.0f) - 1.0f) * 0.5f);
-        i = (i + 1) * (i + 2) / 2 <= ee ? i + 1 : (i * (i + 1) / 2 > ee ? i - 1 : i);
-        const int j = ee - i * (i + 1) / 2, ic = i < 12 ? i : 11, jc = j < 12 ? j : 11;
-        const double* G = Gs + AF3_PC * q;
-        const double rq = q == 0 ? req[0] : (q == 1 ? req[1] : req[2]);
-        const double pq = G[120 + 6 * (i < 6 ? i : 0) + (j < 6 ? j : 0)];
-        const double pd = G[156 + i];
-        const double ib = G[174 + ic];
-        const double dj = adm_dot2<12>(0.0, sm.J[q] + i, 18, sm.J[q] + j, 18);
-        const double dc = adm_dot2<18>(0.0, sm.Cp[q] + FS * ic, 1, sm.Cp[q] + FS * jc, 1);
-        double v = i < 6 && j < 6 ? pq : (i == j && i >= 6 ? pd : 0.0);
-        if (i == j) v += sigma;
-        if (i == j && i < 12) v += rq * (ib * ib);
-        if (k < N - 1) v += rq * dj;
-        if (k > 0 && i < 12 && j < 12) v -= dc;
-        if (i >= nk || j >= nk) v = i == j ? 1.0 : 0.0;
-        sm.S[q][FS * i + j] = v;
-        sm.S[q][FS * j + i] = v;
-      }
-    }
-    wave_sync();
-    double r[18];
-#pragma unroll
-    for (int j = 0; j < 18; ++j) r[j] = sm.S[gl][FS * lr + j];
-    double myid = 1.0;
-#pragma unroll
-    for (int p = 0; p < 18; ++p) {
-      // the pivot of every group (lane 21 g + p) by readlane, this lane's group's selected
-      const double p0 = adm_readlane(r[p], p), p1 = adm_readlane(r[p], AF3_W + p), p2 = adm_readlane(r[p], 2 * AF3_W + p);
-      const double d = sqrt(gl == 0 ? p0 : (gl == 1 ? p1 : p2));
-      const double id = 1.0 / d;
-      myid = li == p ? id : myid;
-      r[p] = li == p ? d : (li > p ? r[p] * id : r[p]);
-      if (p < 17) {
-        double* col = sm.col[gl] + 32 * (p & 1);
-        if (li < 18) col[li] = r[p];
-        wave_sync();
-#pragma unroll
-        for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
-      }
-    }
-    wave_sync();
-    if (li < 18) {
-#pragma unroll
-      for (int j = 0; j < 18; ++j) sm.S[gl][FS * li + j] = r[j];
-      sm.S[gl][FS * li + 18] = myid;
-    }
-    wave_sync();
-    double x[18];
-    const double* Sg = sm.S[gl];
-#pragma unroll
-    for (int i = 0; i < 18; ++i) {
-      int o = FS * i;
-      if (i >= 2) asm volatile("" : "+v"(o) : "v"(x[i - 2]));
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < i; ++q) acc += Sg[o + q] * x[q];
-      x[i] = ((i == lr ? 1.0 : 0.0) - acc) * Sg[o + 18];
-    }
-    if (li < 18) {
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        const double v = i < nk && li < nk ? x[i] : 0.0;
-        sm.L[gl][18 * i + li] = v;
-        if (li < adm_lw(i)) a5_st(v, rA, oRec + 8u * (unsigned)(ADM_REC * k + adm_lrec(i, li)));
-      }
-    }
-    wave_sync();
-    if (k < N - 1) {
-#pragma unroll 1
-      for (int t = 0; t < 11; ++t) {
-        const int e = l + 64 * t;
-        if (e < AF3_G * 216) {
-          const int q = e / 216, ee = e - 216 * q, i = ee / 18, j = ee - 18 * i;
-          const double rq = q == 0 ? req[0] : (q == 1 ? req[1] : req[2]);
-          const double acc = adm_dot2<18>(0.0, sm.J[q] + 18 * i, 1, sm.L[q] + 18 * j, 1);
-          const double cv = rq * (Gs + AF3_PC * q)[186 + i] * acc;
-          sm.Cp[q][FS * i + j] = cv;
-        }
-      }
-    }
-    wave_sync_fence();
-  }
-}
-
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_SCALE_WPE, I7M_ADMM_SCALE_WPE)))
 k_admm_scale(AdmmArgs a) {
@@ -1674,11 +1489,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
 }
-// three problems per wave (grid = ceil(problems / 3)); one wave per SIMD (LDS)
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_factor3(AdmmArgs a) {
-  __shared__ AdmF3Lds sm;
-  adm_factor3(a, sm);
-}
+
 // four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {

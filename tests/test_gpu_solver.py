@@ -228,17 +228,34 @@ def test_goal_stride_6_equals_stride_3(lib, model):
     np.testing.assert_array_equal(o3, o6)
 
 
-def test_sharded_solver_matches_single(lib, model):
+@pytest.mark.parametrize("mode", ["admm", "direct"])
+def test_sharded_solver_matches_single(lib, model, mode):
+    """ShardedSQP (one host thread per device; here both shards on device 0) = one handle, bit for
+    bit, in the drop-in default (ADMM: over two consecutive calls, so each shard carries its
+    problems' OSQP state; the gathered state equals the single handle's) and in the exact mode.  In
+    ADMM mode another batch size is refused until reset() (it would move problems across shards)."""
     from indy7_mpc_amd.sharding import ShardedSQP
 
     N, B = 16, 10
     xcur, goals, XU = synthetic_batch(B, N, seed=15)
-    sh = ShardedSQP(model, devices=[0, 0], N=N, max_batch_per_device=8)
-    out, st = sh.solve(xcur, goals, XU)
-    h = lib.Handle(model, N=N, max_batch=B)
-    ref, rst = h.solve(xcur, goals, XU)
-    np.testing.assert_array_equal(out, ref)
-    np.testing.assert_array_equal(st["qp_iters"], rst["qp_iters"])
+    sh = ShardedSQP(model, devices=[0, 0], N=N, max_batch_per_device=8, qp_mode=mode)
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM if mode == "admm" else lib.QP_DIRECT)
+    xin, rin = XU, XU
+    for _ in range(2 if mode == "admm" else 1):
+        out, st = sh.solve(xcur, goals, xin)
+        ref, rst = h.solve(xcur, goals, rin)
+        np.testing.assert_array_equal(out, ref)
+        np.testing.assert_array_equal(st["qp_iters"], rst["qp_iters"])
+        xin, rin = out, ref
+    if mode == "admm":
+        for a, b in zip(sh.admm_state(B), h.admm_state(B)):
+            np.testing.assert_array_equal(a, b)
+        with pytest.raises(ValueError, match="reset"):
+            sh.solve(xcur[:6], goals[:6], XU[:6])
+        sh.reset()
+        again, _ = sh.solve(xcur[:6], goals[:6], XU[:6])
+        h6 = lib.Handle(model, N=N, max_batch=6, qp_mode=lib.QP_ADMM)
+        np.testing.assert_array_equal(again, h6.solve(xcur[:6], goals[:6], XU[:6])[0])
 
 
 def test_errors_are_loud(lib, model):
