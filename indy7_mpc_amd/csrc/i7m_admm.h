@@ -75,9 +75,6 @@ struct AdmmArgs {
 #ifndef I7M_ADMM_FACTOR
 #define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
-#ifndef I7M_ADMM_CHOL_OVERLAP
-#define I7M_ADMM_CHOL_OVERLAP 1  // the factor's pivot column to LDS unscaled, under the pivot's sqrt / reciprocal
-#endif
 #ifndef I7M_ADMM_SCALE_WPE
 #define I7M_ADMM_SCALE_WPE 2  // (N <= 32: the linearisation magnitudes stay in registers for all ten passes)
 #endif
@@ -680,30 +677,17 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     double myid = 1.0;  // 1 / L_ll of this lane's row (the inverse multiplies by it)
 #pragma unroll
     for (int p = 0; p < 18; ++p) {
-#if I7M_ADMM_CHOL_OVERLAP
-      // column p goes to LDS UNSCALED, before the pivot's square root and reciprocal, so its round
-      // trip runs under them; a reader scales the entry itself (col[j] * id is the product the
-      // writing lane formed before, the same two operands: bit-identical)
-      double* col = sCol + 32 * (p & 1);
-      if (p < 17 && l < 18) col[l] = r[p];
-#endif
       const double d = sqrt(adm_readlane(r[p], p));
       const double id = 1.0 / d;
       myid = l == p ? id : myid;
       r[p] = l == p ? d : (l > p ? r[p] * id : r[p]);
       if (p < 17) {
-#if I7M_ADMM_CHOL_OVERLAP
-        wave_sync();
-#pragma unroll
-        for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * (col[j] * id);
-#else
         // column p of L to the wave through LDS (double-buffered: no wait for the last reads)
         double* col = sCol + 32 * (p & 1);
         if (l < 18) col[l] = r[p];
         wave_sync();
 #pragma unroll
         for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
-#endif
       }
     }
     wave_sync();  // every lane has read S before L overwrites it
@@ -1489,7 +1473,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
 }
-
 // four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {
