@@ -587,8 +587,13 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
   const BoxParams BP = box_params(h);
   const dim3 g(P.B), blk(64);
   if (h->ipm_mode != 2) {
+#ifdef I7M_DIAG
+    const IpmFusedArgs fa{h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf, sol, sol,
+                          W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst, W.bact, W.bhinv, W.bdh, h->ablate};
+#else
     const IpmFusedArgs fa{h->d_model, P, BP, xu, xs, W.lin, W.cost, W.qpd, active, W.kbuf, sol, sol,
                           W.bx, W.bzl, W.bzu, W.bsig, W.bh, W.bdxa, W.bst, W.bact, W.bhinv, W.bdh};
+#endif
     rc = timed(h, s, I7M_K_IPM_FUSED, [&](hipEvent_t ea, hipEvent_t eb) {
       if (h->ipm_mode == 0)
         hipExtLaunchKernelGGL(k_ipm_fused<true>, g, blk, 0, s, ea, eb, 0, fa);

@@ -446,7 +446,15 @@ struct IpmFusedArgs {
   IpmState* st;
   int* ipm_active;
   double *hinv, *dh;
+#ifdef I7M_DIAG
+  // I7M_ABLATE (diagnostic timing builds only, results invalid): 40 every problem runs exactly
+  // IPM_ABL_IT interior-point iterations (convergence ignored), 41 + the predictor's element passes
+  // skipped, 42 + the corrector's, 43 + both (Newton steps only), 44 + the Newton steps skipped
+  // (element passes only) — the per-iteration cost of each part at a fixed iteration count
+  int ablate;
+#endif
 };
+constexpr int IPM_ABL_IT = 7;
 // the kernarg segment, laundered (the cast back to a generic pointer is inferred to the
 // constant address space again, so the fields are scalar loads)
 __device__ __forceinline__ const IpmFusedArgs* kernarg_ipm() {
@@ -477,13 +485,21 @@ k_ipm_fused(IpmFusedArgs args) {
   // treat as redefining them): the Riccati operand maps, the box bounds and the buffer pointers
   // are rebuilt / reloaded per step instead of hoisted out of the loop and held live across it.
   // !DELTA: one Riccati call site (half 0: predictor, half 1: corrector) keeps one inlined copy.
+#ifdef I7M_DIAG
+  const int abl = args.ablate;
+  const bool skip_newton = abl == 44, skip_pred = abl == 41 || abl == 43, skip_corr = abl == 42 || abl == 43;
+#else
+  constexpr int abl = 0;
+  constexpr bool skip_newton = false, skip_pred = false, skip_corr = false;
+#endif
   for (int half = 0; run; half ^= 1) {
     int l = threadIdx.x;
     const IpmFusedArgs* A = kernarg_ipm();
     asm volatile("" : "+v"(l));
     const SolveParams P = A->P;
     __syncthreads();
-    if (!DELTA) {
+    if (skip_newton) {
+    } else if (!DELTA) {
       // the corrector (half 1) stores only K~'s feedforward column: its gain is the predictor's
       riccati_mfma_body<0, true, false, I7M_IPM_BC>(b, P, A->xu, A->xs, A->lin, A->cost, A->qpd, A->kbuf, A->y, A->sig,
                                                     A->h, sh, l, nullptr, half == 1);
@@ -499,12 +515,18 @@ k_ipm_fused(IpmFusedArgs args) {
     // the most work left first: remaining iterations ~ log(mu / tol) (mu_0 = z0 = 0.1, tol 1e-8)
     if (I7M_PRIO & 4) set_prio((int)(log10(fmax(S.mu / BP.tol, 1.0)) * (1.0 / 2.5)));
     if (half == 0) {
-      ipm_pred_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
-      ipm_uniform(S);
+      if (!skip_pred) {
+        ipm_pred_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->h, S, DELTA ? B->dh : nullptr);
+        ipm_uniform(S);
+      }
     } else {
-      ipm_corr_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->sig, B->h, S);
-      ipm_uniform(S);
-      run = !ipm_done(S, BP);
+      if (!skip_corr) {
+        ipm_corr_body(Bt, B->P, BP, b, B->y, B->x, B->zl, B->zu, B->dxa, B->sig, B->h, S);
+        ipm_uniform(S);
+      } else {
+        S.iters += 1;
+      }
+      run = abl >= 40 ? S.iters < IPM_ABL_IT : !ipm_done(S, BP);
     }
   }
   if (threadIdx.x == 0) {
