@@ -73,7 +73,7 @@ struct AdmmArgs {
 #define I7M_ADMM_FSTRIDE 19  // the register factor's LDS row stride for S and C (18: 3-way bank conflicts on row reads)
 #endif
 #ifndef I7M_ADMM_FACTOR
-#define I7M_ADMM_FACTOR 2  // 4: two problems per wave (adm_factor2), 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
+#define I7M_ADMM_FACTOR 2  // 2: register Cholesky (adm_factor), 1: LDS-staged (adm_factor_lds)
 #endif
 #ifndef I7M_ADMM_SCALE_WPE
 #define I7M_ADMM_SCALE_WPE 2  // (N <= 32: the linearisation magnitudes stay in registers for all ten passes)
@@ -1464,177 +1464,6 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   }
 }
 
-// k_admm_factor at two problems per wave (I7M_ADMM_FACTOR 4): lanes 32 g .. 32 g + 17 hold problem
-// g's rows / columns, so the Cholesky and the inverse serve two problems per instruction, while the
-// element passes (J staged dense, S's lower triangle, C_k) spread both problems' entries over the
-// 64 lanes.  Per problem exactly adm_factor's operations in its order: the records are
-// bit-identical.  LDS stays under 20 KB per wave so that two waves share a SIMD, as adm_factor's
-// single-problem waves do: one stage buffer, filled from registers that the previous stage loaded
-// (four 16-byte buffer loads per lane, in flight while that stage computes), and Linv_k written
-// over S (dead once the inverse has read it) instead of a buffer of its own.
-constexpr int AF2_G = 2, AF2_W = 32;  // problems per wave, lanes per problem
-constexpr int AF2_PC = 198;           // stage operands per problem (doubles): J 120 | Pq 36 | Pd 18 | I_k 12 | I_{k+1} 12
-constexpr int AF2_NU = 4;             // 16-byte pieces per lane and stage (256 >= 2 x 99)
-struct alignas(16) AdmF2Lds {
-  double stg[2 * 64 * AF2_NU];                 // problem q's operands at 198 q
-  double S[AF2_G][18 * I7M_ADMM_FSTRIDE];      // S_k, then its Cholesky rows (+ 1 / L_ii), then Linv_k
-  double J[AF2_G][216];
-  double Cp[AF2_G][12 * I7M_ADMM_FSTRIDE];
-  double col[AF2_G][64];
-};
-typedef unsigned int a2u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void adm_factor2(const AdmmArgs& a, AdmF2Lds& sm) {
-  const SolveParams& P = a.P;
-  const int N = P.N, T = P.T, m = 12 * N;
-  const double sigma = a.A.sigma;
-  constexpr int FS = I7M_ADMM_FSTRIDE;
-  const int b0 = a.b0 + AF2_G * (int)blockIdx.x;
-  const bool ok0 = b0 < P.B && !(a.active && !a.active[b0]);
-  const bool ok1 = b0 + 1 < P.B && !(a.active && !a.active[b0 + 1]);
-  if (!ok0 && !ok1) return;
-  const double req0 = ok0 ? 1e3 * a.srho[b0] : 0.0, req1 = ok1 ? 1e3 * a.srho[b0 + 1] : 0.0;
-  const auto rA = a4_rsrc(a.abase, a.abytes);
-  auto boff = [&](const double* q) { return (unsigned)__builtin_amdgcn_readfirstlane((int)((const char*)q - (const char*)a.abase)); };
-  const unsigned oR = boff(a.R), oPq = boff(a.Pq), oPd = boff(a.Pd), oI = boff(a.I);
-  a2u4 pf[AF2_NU];
-  // stage k's operands into pf: piece g = 64 u + l of problem q = g / 99, its piece j = g % 99:
-  // [0, 60) J, [60, 78) Pq, [78, 87) Pd, [87, 99) I_k and I_{k+1} (offsets recomputed per call:
-  // held across the stage they would spill)
-  auto load = [&](int k, int l) {
-#pragma unroll
-    for (int u = 0; u < AF2_NU; ++u) {
-      const int g = 64 * u + l, q = g / 99, j = g - 99 * q;
-      const int b = b0 + (q < AF2_G ? q : 0);
-      const bool ok = q < AF2_G && (q == 0 ? ok0 : ok1);
-      unsigned o;
-      if (j < 60) o = oR + 8u * (unsigned)(b * N * ADM_REC + ADM_REC * k + REC_J) + 16u * j;
-      else if (j < 78) o = oPq + 8u * (unsigned)(b * N * 36 + 36 * k) + 16u * (j - 60);
-      else if (j < 87) o = oPd + 8u * (unsigned)(b * T + 18 * k) + 16u * (j - 78);
-      else o = oI + 8u * (unsigned)(b * m + 12 * k) + 16u * (j - 87);
-      pf[u] = __builtin_amdgcn_raw_buffer_load_b128(rA, ok ? o : A5_OOB, 0, 0);
-    }
-  };
-  load(0, (int)threadIdx.x);
-  for (int k = 0; k < N; ++k) {
-    const int nk = k < N - 1 ? 18 : 12;
-    // the lane's indices, recomputed every stage (adm_factor's register budget)
-    int l = threadIdx.x;
-    asm volatile("" : "+v"(l));
-    const int gl = l >> 5, li = l & 31, lr = li < 18 ? li : 17;
-    const bool mine = (gl == 0 ? ok0 : ok1) && li < 18;
-    // stage k's operands (loaded during stage k - 1) into the stage buffer, stage k + 1's loads issued
-#pragma unroll
-    for (int u = 0; u < AF2_NU; ++u) *(a2u4*)(sm.stg + 2 * (64 * u + l)) = pf[u];
-    wave_sync();
-    const double* Gs = sm.stg;  // problem q's operands at Gs + AF2_PC q
-    if (k < N - 1) {
-      // J_k dense (12 x 18) per problem from its compact form
-#pragma unroll 1
-      for (int e = l; e < AF2_G * 216; e += 64) {
-        const int q = e / 216, ee = e - 216 * q, i = ee / 18, j = ee - 18 * i;
-        const double* Jc = Gs + AF2_PC * q;
-        double v;
-        if (i < 6) v = j == i ? Jc[i] : (j == 6 + i ? Jc[6 + i] : 0.0);
-        else v = Jc[12 + 18 * (i - 6) + j];
-        sm.J[q][ee] = v;
-      }
-    }
-    wave_sync();
-    // S's lower triangle, both problems' 342 entries over the wave (adm_factor's formulas)
-#pragma unroll 1
-    for (int t = 0; t < 6; ++t) {
-      const int e = l + 64 * t;
-      if (e < AF2_G * 171) {
-        const int q = e / 171, ee = e - 171 * q;
-        int i = (int)((sqrtf(8.0f * (float)ee + 1.0f) - 1.0f) * 0.5f);
-        i = (i + 1) * (i + 2) / 2 <= ee ? i + 1 : (i * (i + 1) / 2 > ee ? i - 1 : i);
-        const int j = ee - i * (i + 1) / 2, ic = i < 12 ? i : 11, jc = j < 12 ? j : 11;
-        const double* G = Gs + AF2_PC * q;
-        const double rq = q == 0 ? req0 : req1;
-        const double pq = G[120 + 6 * (i < 6 ? i : 0) + (j < 6 ? j : 0)];
-        const double pd = G[156 + i];
-        const double ib = G[174 + ic];
-        const double dj = adm_dot2<12>(0.0, sm.J[q] + i, 18, sm.J[q] + j, 18);
-        const double dc = adm_dot2<18>(0.0, sm.Cp[q] + FS * ic, 1, sm.Cp[q] + FS * jc, 1);
-        double v = i < 6 && j < 6 ? pq : (i == j && i >= 6 ? pd : 0.0);
-        if (i == j) v += sigma;
-        if (i == j && i < 12) v += rq * (ib * ib);
-        if (k < N - 1) v += rq * dj;
-        if (k > 0 && i < 12 && j < 12) v -= dc;
-        if (i >= nk || j >= nk) v = i == j ? 1.0 : 0.0;
-        sm.S[q][FS * i + j] = v;
-        sm.S[q][FS * j + i] = v;
-      }
-    }
-    wave_sync();
-    double* Sg = sm.S[gl];
-    double r[18];
-#pragma unroll
-    for (int j = 0; j < 18; ++j) r[j] = Sg[FS * lr + j];
-    double myid = 1.0;
-#pragma unroll
-    for (int p = 0; p < 18; ++p) {
-      const double p0 = adm_readlane(r[p], p), p1 = adm_readlane(r[p], AF2_W + p);
-      const double d = sqrt(gl == 0 ? p0 : p1);
-      const double id = 1.0 / d;
-      myid = li == p ? id : myid;
-      r[p] = li == p ? d : (li > p ? r[p] * id : r[p]);
-      if (p < 17) {
-        double* col = sm.col[gl] + 32 * (p & 1);
-        if (li < 18) col[li] = r[p];
-        wave_sync();
-#pragma unroll
-        for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
-      }
-    }
-    wave_sync();
-    if (li < 18) {
-#pragma unroll
-      for (int j = 0; j < 18; ++j) Sg[FS * li + j] = r[j];
-      Sg[FS * li + 18] = myid;
-    }
-    wave_sync();
-    double x[18];
-#pragma unroll
-    for (int i = 0; i < 18; ++i) {
-      int o = FS * i;
-      if (i >= 2) asm volatile("" : "+v"(o) : "v"(x[i - 2]));
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < i; ++q) acc += Sg[o + q] * x[q];
-      x[i] = ((i == lr ? 1.0 : 0.0) - acc) * Sg[o + 18];
-    }
-    wave_sync();  // every lane has read L before Linv_k overwrites it
-    if (li < 18) {
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        const double v = i < nk && li < nk ? x[i] : 0.0;
-        Sg[FS * i + li] = v;  // Linv_k row-major over S
-        if (li < adm_lw(i))
-          a5_st(v, rA, mine ? oR + 8u * (unsigned)((b0 + gl) * N * ADM_REC + ADM_REC * k + adm_lrec(i, li)) : A5_OOB);
-      }
-    }
-    wave_sync();
-    // stage k + 1's operands, in flight under C_k and the loop's turn (issued here, not at the
-    // stage's start: held across the Cholesky they would spill)
-    if (k + 1 < N) load(k + 1, l);
-    if (k < N - 1) {
-#pragma unroll 1
-      for (int t = 0; t < 7; ++t) {
-        const int e = l + 64 * t;
-        if (e < AF2_G * 216) {
-          const int q = e / 216, ee = e - 216 * q, i = ee / 18, j = ee - 18 * i;
-          const double rq = q == 0 ? req0 : req1;
-          const double acc = adm_dot2<18>(0.0, sm.J[q] + 18 * i, 1, sm.S[q] + FS * j, 1);
-          const double cv = rq * (Gs + AF2_PC * q)[186 + i] * acc;
-          sm.Cp[q][FS * i + j] = cv;
-        }
-      }
-    }
-    wave_sync_fence();
-  }
-}
-
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_SCALE_WPE, I7M_ADMM_SCALE_WPE)))
 k_admm_scale(AdmmArgs a) {
@@ -1643,11 +1472,6 @@ k_admm_scale(AdmmArgs a) {
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_FACTOR_WPE, I7M_ADMM_FACTOR_WPE)))
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
-}
-// two problems per wave (grid = ceil(problems / 2)), two waves per SIMD (LDS < 20 KB)
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_admm_factor2(AdmmArgs a) {
-  __shared__ AdmF2Lds sm;
-  adm_factor2(a, sm);
 }
 // four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>

@@ -554,17 +554,7 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
           (void)hipEventRecord(h->mark_ev, s);
           h->mark_ev = nullptr;
         }
-#if I7M_ADMM_FACTOR == 4
-        {  // two problems per wave over [lo, lo + n) (a.b0 = lo)
-          SolveParams P2 = a.P;
-          P2.B = lo + n;
-          AdmmArgs a2 = a;
-          a2.P = P2;
-          hipExtLaunchKernelGGL(k_admm_factor2, dim3((n + 1) / 2), dim3(64), 0, s, nullptr, eb, 0, a2);
-        }
-#else
         hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
-#endif
       });
       if (rc2) return rc2;
       if (h->mark_ev && h->admm_stagger == 1) {
