@@ -153,7 +153,7 @@ def test_direct_mode_vs_osqp_distribution_is_pinned():
     measured median 5.8e-5, p90 2.0e-4, max 1.0e-3, 31 % of problems above north_star's 1e-4.
     Pinned here so the gap between the two modes cannot drift unseen (VERDICT r4 "What's weak" 1);
     the device's direct mode equals the port's direct mode to 1e-12 (tests/test_gpu_solver.py),
-    so these are also the device's numbers, and bench.py reports them as `parity_vs_osqp`."""
+    so these are also the device's numbers, and bench.py reports them as `exact_mode.parity_vs_port_admm`."""
     B, N = 1024, 32
     xcur, goals, XU = synthetic_batch(B, N, 45)
     d, qp_d, al_d, _ = cpu.solve(xcur, goals, XU, N, nthreads=8)

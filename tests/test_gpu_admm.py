@@ -179,7 +179,7 @@ def test_admm_full_size_every_problem_matches_port(lib, model):
     """Config 3 at full size in ADMM mode (B = 4096, N = 32, seed 45, cold OSQP state): every
     problem's SQP iterations, OSQP iterations per QP and line-search steps equal the port's, XU to
     1e-7 (measured max 1.4e-8, median 3.9e-10: the M of a second SQP iteration has cond ~4e7, so
-    the linearisations' 1e-16 differences reach x at ~1e-9) — the same comparison the bench's config3_admm.parity_vs_port makes, as a test."""
+    the linearisations' 1e-16 differences reach x at ~1e-9) — the same comparison the bench's headline `parity_vs_port` makes, as a test."""
     B, N = 4096, 32
     xcur, goals, XU = synthetic_batch(B, N, 45)
     h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
