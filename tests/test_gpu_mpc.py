@@ -249,3 +249,58 @@ def test_closed_loop_500_steps_admm_default_shadowed_by_port(lib, model):
         got = xs[i + 2] if i < 499 else np.concatenate([ctrl.xpath[-1], np.full(6, np.nan)])
         k = 12 if i < 499 else 6
         assert np.linalg.norm(nxt[:k] - got[:k]) <= 1e-12 * np.linalg.norm(nxt[:k]), i
+
+
+class _PortAdmmSQP:
+    """run_mpc_ref's `sqp` with every solve by the C++ port's ADMM mode, the OSQP state carried from
+    call to call (one instance: the reference's single osqp.OSQP object, src/osqp_solver.py:38-40)."""
+
+    def __init__(self, N=32):
+        from oracle import cpu
+        self.cpu, self.solver, self.N = cpu, OSQPSolverRef(N=N), N
+        self.state = cpu.AdmmState(1, N)
+
+    def sqp(self, xcur, goal, XU):
+        out, *_ = self.cpu.solve_admm(np.asarray(xcur, float)[None], np.asarray(goal, float)[None],
+                                      np.asarray(XU, float)[None], self.N, self.state)
+        return out[0]
+
+
+def test_batched_closed_loop_admm_default_matches_port_runs(lib, model):
+    """MPC_OSQP.run_mpc_batch in the drop-in default (ADMM: every instance's OSQP state carried on the
+    device from MPC step to MPC step, i7m_mpc_run) against an independent closed loop per instance
+    whose SQP is the C++ port's ADMM mode with its own carried state (oracle/mpc_ref.py's loop:
+    goal switching, the > 1.1 stop, rk4 plant, shift and pins of src/osqp_mpc.py:14-72).  The five
+    instances of the direct-mode test: the notebook's start, one that switches goals, one that stops
+    at once, two random.  Goal distances and q paths to 1e-8 over 8 MPC steps (the ADMM loop doubles
+    a rounding-level difference every ~1.5 steps: test_admm_closed_loop_reproduces_notebook); NaN
+    where an instance stopped, at the same step."""
+    from indy7_mpc_amd.osqp_mpc import MPC_OSQP
+    from indy7_mpc_amd.osqp_solver import OSQPSolver
+    from indy7_mpc_amd.osqp_sqp import SQP_OSQP
+
+    tr = json.load(open(os.path.join(GOLD, "notebook_kats.json")))["mpc_trace"]
+    ends = np.array([rbd.eepos(np.array(q)) for q in tr["endpoint_q"]])
+    steps = 8
+    rng = np.random.default_rng(8)
+    xs = np.zeros((5, 12))
+    xs[0] = tr["xstart"]
+    xs[1, :6] = np.array(tr["endpoint_q"][0]) + 0.01
+    xs[2, :6], xs[2, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
+    xs[3, :6] = [0.4, -1.9, -0.6, -2.0, -0.1, 0.4]
+    xs[4, :6], xs[4, 6:] = rng.uniform(-1, 1, 6), rng.uniform(-0.5, 0.5, 6)
+    solver = OSQPSolver(model)
+    assert solver.box["qp_mode"] == lib.QP_ADMM
+    ctrl = MPC_OSQP(model, SQP_OSQP(solver), solver)
+    q, d = ctrl.run_mpc_batch(xs, ends, num_steps=steps)
+    for b in range(5):
+        xpath, dists = run_mpc_ref(_PortAdmmSQP(), xs[b], ends, num_steps=steps)
+        n = len(dists)
+        np.testing.assert_allclose(d[:n, b], dists, rtol=0, atol=1e-8, err_msg=f"instance {b}")
+        assert np.isnan(d[n:, b]).all()
+        n_plant = len(xpath)
+        np.testing.assert_allclose(q[:n_plant, b], np.array(xpath).reshape(n_plant, 6), rtol=0, atol=1e-8)
+        assert np.isnan(q[n_plant:, b]).all()
+    assert np.isnan(d[1:, 3]).all() and d[0, 3] > 1.1
+    # the notebook's instance meets the reference's printed distances (its OSQP run)
+    assert np.abs(d[:, 0] - np.array(tr["goal_distances"][:steps])).max() < 2e-9
