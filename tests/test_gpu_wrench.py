@@ -220,3 +220,34 @@ def test_batch_sqp_default_admm_world_wrench_matches_port(lib, model):
     # the wrench is in the solve: the zero-wrench row 0 against a plain ADMM handle's first call
     # is covered by the port comparison; here the hypotheses must actually differ
     assert not np.allclose(out[1], out[2])
+
+
+@pytest.mark.parametrize("frame", ["world", "local"])
+def test_admm_wrench_handle_matches_port(lib, model, frame):
+    """ADMM mode with a per-problem joint-6 wrench in either frame through the C-ABI (Handle, the
+    layer under batch_sqp) against the C++ port's ADMM mode with the same wrench and frame, two
+    consecutive solves (the OSQP state carried): OSQP iterations, statuses and alphas identical, XU
+    5e-8."""
+    from oracle import cpu
+
+    N, B = 16, 12
+    xcur, goals, XU = synthetic_batch(B, N, seed=19)
+    f = np.random.default_rng(4).normal(0, 25, (B, 6))
+    f[:, 3:] *= 0.05
+    h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+    h.set_external_wrench(f, frame)
+    st = cpu.AdmmState(B, N)
+    xin = XU
+    for call in range(2):
+        out, s = h.solve(xcur, goals, xin)
+        it, _, stat = h.admm_stats(B, with_status=True)
+        ref, qp, al, _, it_r = cpu.solve_admm(xcur, goals, xin, N, st, fext=f, fext_frame=frame)
+        np.testing.assert_array_equal(s["qp_iters"], qp)
+        ran = np.arange(8)[None, :] < qp[:, None]
+        np.testing.assert_array_equal(np.where(ran, it, -1), np.where(ran, it_r, -1))
+        np.testing.assert_array_equal(np.where(ran, stat, -9), np.where(ran, st.status, -9))
+        for b in range(B):
+            np.testing.assert_array_equal(s["alphas"][b, :s["n_alphas"][b]], al[b, :qp[b]])
+        rel = np.linalg.norm(out - ref, axis=1) / np.linalg.norm(ref, axis=1)
+        assert rel.max() < 5e-8, (call, rel.max())
+        xin = out
