@@ -148,6 +148,7 @@ struct i7m_handle {
   int admm_stagger = 1;
   int stagger_modes = 1 << I7M_QP_ADMM;  // the QP modes that stagger (bit per mode; I7M_STAGGER_MODES)
   int admm_ranges = 2;
+  int admm_chains = 1;  // ranges r wait for range r - chains's mark (I7M_ADMM_CHAINS, A/B: 2 = two independent stagger chains)
   int admm_split = 500;  // two ranges: the first's share of the batch, per mille (I7M_ADMM_SPLIT, A/B)
   int admm_stagger_min_b = 3072;  // measured, two ranges: B = 8192 / 4096 / 3072 +9 / +17 / +5 %; 2048 / 1024 -8 / -11 %
   static constexpr int kMaxRanges = 4;
@@ -1123,6 +1124,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_STAGGER_MODES")) h->stagger_modes = std::atoi(e);
   if (const char* e = std::getenv("I7M_ADMM_RANGES"))
     h->admm_ranges = std::min(std::max(std::atoi(e), 1), (int)i7m_handle::kMaxRanges);
+  if (const char* e = std::getenv("I7M_ADMM_CHAINS")) h->admm_chains = std::min(std::max(std::atoi(e), 1), 2);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||
@@ -1383,18 +1385,18 @@ static int run_staggered(i7m_handle* h, int B, Body&& body) {
     return std::min<long>(std::max<long>(c, 0), B);
   };
   HIPCHK(hipEventRecord(h->ev_order, h->stream));
-  bool prev_marked = false;
+  // range r starts behind range r - C's mark (C = admm_chains: 1 one chain of ranges, 2 two
+  // interleaved chains started together)
+  const int C = std::min(h->admm_chains, R);
+  bool marked[i7m_handle::kMaxRanges] = {};
   for (int r = 0; r < R; ++r) {
     const long lo = cut(r), hi = cut(r + 1);
     HIPCHK(hipStreamWaitEvent(ss[r], h->ev_order, 0));
-    if (hi <= lo) {
-      prev_marked = false;
-      continue;
-    }
-    if (prev_marked) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - 1], 0));
-    h->mark_ev = r + 1 < R ? h->ev_rmark[r] : nullptr;
+    if (hi <= lo) continue;
+    if (r >= C && marked[r - C]) HIPCHK(hipStreamWaitEvent(ss[r], h->ev_rmark[r - C], 0));
+    h->mark_ev = r + C < R ? h->ev_rmark[r] : nullptr;
     const int rc = body(lo, (int)(hi - lo), ss[r]);
-    prev_marked = r + 1 < R && !h->mark_ev;
+    marked[r] = r + C < R && !h->mark_ev;
     h->mark_ev = nullptr;
     if (rc) {
       // join the ranges already started back into h->stream before the error returns:
