@@ -1099,19 +1099,47 @@ __device__ __forceinline__ void a5_dma(__amdgpu_buffer_rsrc_t r, unsigned lds, c
 // the step's slot has landed: at most 13 vector-memory operations in flight (the next step's DMA,
 // or the stores issued after its first ones: every operation completes in issue order)
 __device__ __forceinline__ void a5_wait() { asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); }
+// two problems per wave (k_admm_iter2): 5 record and 2 vector wave-instructions per step
+__device__ __forceinline__ void a5_dma2(__amdgpu_buffer_rsrc_t r, unsigned lds, const unsigned (&ro)[5], unsigned so,
+                                        const unsigned (&vo)[2]) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %9, %10 offen lds\n\t"
+      "buffer_load_dwordx4 %3, %9, %10 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %4, %9, %10 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %5, %9, %10 offen offset:3072 lds\n\t"
+      "s_add_u32 m0, m0, 0x1000\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %9, %10 offen lds\n\t"
+      "buffer_load_dwordx4 %7, %9, 0 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %8, %9, 0 offen offset:2048 lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(ro[0]), "v"(ro[1]), "v"(ro[2]), "v"(ro[3]), "v"(ro[4]),
+        "v"(vo[0]), "v"(vo[1]), "s"(r), "s"(__builtin_amdgcn_readfirstlane(so))
+      : "memory");
+}
+__device__ __forceinline__ void a5_wait2() { asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); }
 __device__ __forceinline__ void a5_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// OSQP's iteration loop of one wave (four problems).  Per-lane state lives in registers.
-template <bool ADAPT>
+// OSQP's iteration loop of one wave (PW problems: 4, or 2 in k_admm_iter2, whose rows 2 and 3 idle
+// so that the ring takes 21 KB and two waves can share a SIMD).  Per-lane state lives in registers.
+template <bool ADAPT, int PW = 4>
 __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
+  static_assert(PW == 4 || PW == 2, "four or two problems per wave");
+  constexpr int RI = PW == 4 ? A5_RI : 5, VI = PW == 4 ? A5_VI : 2;  // record / vector DMA wave-instructions
+  constexpr int SLOT = 64 * (RI + VI), VD = 2 * 64 * RI;
+  constexpr int PL = PW - 1;  // the last real row (idle rows read its slot data)
   const SolveParams& P = a.P;
   const int N = P.N, T = P.T, m = 12 * N;
   const int l = threadIdx.x, p = l >> 4, c = l & 15;
-  __shared__ double2 sRing[3 * A5_SLOT];
+  __shared__ double2 sRing[3 * SLOT];
   double* const ring = (double*)sRing;
   const unsigned ring_lds = (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)sRing;
-  const int bb = a.b0 + 4 * (int)blockIdx.x;
-  bool run = bb + p < P.B && !(a.active && !a.active[bb + p]);
+  const int bb = a.b0 + PW * (int)blockIdx.x;
+  bool run = p < PW && bb + p < P.B && !(a.active && !a.active[bb + p]);
   const bool act = run;
   if (!__ballot(run)) return;
   const int bown = bb + p;
@@ -1134,14 +1162,14 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   // DMA source offsets of this lane's pieces (rows that do not run read nothing: out of range).
   // Records: piece g = 64 t + l of the four problems' 632; vectors: piece g = 64 u + l of their
   // 168, problem g / 42 piece j = g % 42: [0, 9) v0, [9, 18) v1, [18, 42) z, y, l, I (6 each).
-  unsigned ro[A5_RI], vF[A5_VI], vB[A5_VI], vD[A5_VI], vZ[A5_VI], vo[A5_VI];
-  int vcls[A5_VI];
+  unsigned ro[RI], vF[VI], vB[VI], vD[VI], vZ[VI], vo[VI];
+  int vcls[VI];
   auto offsets = [&]() {
     const unsigned long long rm = __ballot(run);
 #pragma unroll
-    for (int t = 0; t < A5_RI; ++t) {
+    for (int t = 0; t < RI; ++t) {
       const int g = 64 * t + l, q = g / A5_RP, j = g - A5_RP * q;
-      const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
+      const bool ok = q < PW && ((rm >> (16 * q)) & 1);
       // LDS piece j of the record -> its piece in HBM (rows 0-15 from width 4 to the stored even
       // width: the pieces past it read as zeros)
       int hp;
@@ -1157,9 +1185,9 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       ro[t] = (ok && hp >= 0 ? oR + 8u * (unsigned)((bb + q) * N * ADM_REC) + 16u * hp : A5_OOB) - a5_dma_off(t);
     }
 #pragma unroll
-    for (int u = 0; u < A5_VI; ++u) {
+    for (int u = 0; u < VI; ++u) {
       const int g = 64 * u + l, q = g / A5_VP, j = g - A5_VP * q;
-      const bool ok = q < 4 && ((rm >> (16 * q)) & 1);
+      const bool ok = q < PW && ((rm >> (16 * q)) & 1);
       const unsigned rT = 8u * (unsigned)((bb + q) * T), rM = 8u * (unsigned)((bb + q) * m);
       unsigned f, bk;
       int cl;
@@ -1172,7 +1200,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
         f = (w == 0 ? oZ + 0u : w == 1 ? oY + 0u : w == 2 ? oL + 0u : oI + 0u) + rM + 16u * (jj - 6 * w);
         bk = f; cl = w == 0 ? 3 : 2;
       }
-      const unsigned o = a5_dma_off(A5_RI + u);
+      const unsigned o = a5_dma_off(RI + u);
       vF[u] = (ok ? f : A5_OOB) - o;
       vB[u] = (ok ? bk : A5_OOB) - o;
       vD[u] = ok ? (cl < 2 ? 144u : 96u) : 0u;  // bytes per stage
@@ -1191,7 +1219,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const int k1 = k + 1 < N ? k + 1 : N - 1;
     const int kb = fwd ? k : k1;
 #pragma unroll
-    for (int u = 0; u < A5_VI; ++u) {
+    for (int u = 0; u < VI; ++u) {
       const unsigned st = vcls[u] == 0 ? 144u * k : (vcls[u] == 1 ? 144u * kb : 96u * k1);
       vo[u] = (fwd ? vF[u] + 0u : vB[u] + 0u) + (zl ? vZ[u] + st : st);
     }
@@ -1205,7 +1233,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       vfull(s, zl);
     } else {
 #pragma unroll
-      for (int u = 0; u < A5_VI; ++u) vo[u] = fwd ? vo[u] + vD[u] : vo[u] - vD[u];
+      for (int u = 0; u < VI; ++u) vo[u] = fwd ? vo[u] + vD[u] : vo[u] - vD[u];
     }
 #ifdef I7M_DIAG
     // I7M_ABLATE 21: every step reads stage 0's record (L2-resident: the sweep without its stream)
@@ -1213,7 +1241,10 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
 #else
     const unsigned so = 8u * (unsigned)(k * ADM_REC);
 #endif
-    a5_dma(rA, ring_lds + 16u * A5_SLOT * slot, ro, so, vo);
+    if constexpr (PW == 4)
+      a5_dma(rA, ring_lds + 16u * SLOT * slot, ro, so, vo);
+    else
+      a5_dma2(rA, ring_lds + 16u * SLOT * slot, ro, so, vo);
   };
   issue(0, 0, false);
   issue(1, 1, false);
@@ -1240,14 +1271,17 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   // the step's vectors (rows ci of v0, cb of v1: the last stage's 12 rows clamped) and the first
   // two coefficient sets
   auto begin = [&](int s, int slot, int ci, int cb) {
-    a5_wait();
+    if constexpr (PW == 4)
+      a5_wait();
+    else
+      a5_wait2();
     int sn = s + 2, sl = slot + 2;
     if (sn >= 2 * N) sn -= 2 * N;
     if (sl >= 3) sl -= 3;
     issue(sn, sl, it > 1 || sn < s);
-    const double* S = ring + 2 * A5_SLOT * slot;
-    R = S + A5_LREC * p;
-    const double* V = S + A5_VD + 2 * A5_VP * p;  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
+    const double* S = ring + 2 * SLOT * slot;
+    R = S + A5_LREC * (p < PW ? p : PL);
+    const double* V = S + VD + 2 * A5_VP * (p < PW ? p : PL);  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
     v0 = V[ci];
     v1 = V[18 + cb];
     hv0 = make_double2(V[16], V[17]);
@@ -1404,7 +1438,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
           }
           // re-factor the rows whose rho moved, one problem at a time on the whole wave (the
           // ring is the factor's scratch)
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < PW; ++q) {
             if (!((mv >> (16 * q)) & 0xffff)) continue;
             const long bq2 = bb + q;
             const double rq = __shfl(rho, 16 * q, 64);
@@ -1477,6 +1511,11 @@ k_admm_factor(AdmmArgs a) {
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {
   admm_iter4<ADAPT>(a);
+}
+// two problems per wave (grid = ceil(problems / 2), I7M_ADMM_ITER2 A/B): a 21 KB ring, so that two
+// waves (of one range or of both staggered ranges) can share a SIMD
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_admm_iter2(AdmmArgs a) {
+  admm_iter4<false, 2>(a);
 }
 
 }  // namespace i7m
