@@ -1512,8 +1512,10 @@ template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {
   admm_iter4<ADAPT>(a);
 }
-// two problems per wave (grid = ceil(problems / 2), I7M_ADMM_ITER2 A/B): a 21 KB ring, so that two
-// waves (of one range or of both staggered ranges) can share a SIMD
+// two problems per wave (grid = ceil(problems / 2)): a 21 KB ring, two waves per SIMD possible.  Per
+// problem the same arithmetic (bit-identical); a step issues 7 DMA wave-instructions instead of 13,
+// so a wave's step is shorter when the batch is small (launches of <= 512 problems use it), while
+// at B = 4096 the doubled instruction count per problem costs more than the second wave hides
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_admm_iter2(AdmmArgs a) {
   admm_iter4<false, 2>(a);
 }

@@ -368,3 +368,23 @@ def test_admm_status_after_max_iter_matches_port(lib, model, max_iter, eps):
     assert [QPSolution.from_admm(None, c, 1, None).info.status_val for c in (1, 2, 0)] == [1, 2, -2]
     with pytest.raises(RuntimeError, match="no OSQP result"):
         QPSolution.from_admm(None, -1, 0, None)
+
+
+@pytest.mark.parametrize("B", [13, 600])
+def test_admm_iter_two_and_four_problems_per_wave_bit_identical(lib, model, monkeypatch, B):
+    """k_admm_iter2 (two problems per wave, used for launches of <= 512 problems) and k_admm_iter
+    (four) run the same arithmetic per problem: two consecutive solves with each forced
+    (I7M_ADMM_ITER2 = 1 / 0) are equal bit for bit, carried state, OSQP records and statuses
+    included (B = 13: empty rows in the last wave of both)."""
+    N = 32
+    xcur, goals, XU = synthetic_batch(B, N, 54)
+    res = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("I7M_ADMM_ITER2", mode)
+        h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+        o1, _ = h.solve(xcur, goals, XU)
+        o2, _ = h.solve(xcur, goals, o1)
+        res.append((o1, o2) + h.admm_state(B) + h.admm_stats(B, with_status=True))
+        h.close()
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
