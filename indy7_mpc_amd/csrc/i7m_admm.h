@@ -1139,6 +1139,25 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   double* const ring = (double*)sRing;
   const unsigned ring_lds = (unsigned)(unsigned long)(__attribute__((address_space(3))) void*)sRing;
   const int bb = a.b0 + PW * (int)blockIdx.x;
+#ifdef I7M_DIAG
+  // I7M_ABLATE 100000 + 100 IT + S (tools/step_stamps.py): s_memtime (shader cycles) at nine points
+  // of sweep step S of OSQP iteration IT in workgroup 0, to the timeline buffer's record area 5
+  // (stamps fenced by sched barriers: read the shares, not the length)
+  const int tr_it = a.ablate >= 100000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
+  const bool tr_on = tr_it >= 0 && blockIdx.x == 0;
+  unsigned long long tr_t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int tr_cur = -1;
+#define A5_STAMP(i)                                                                         \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long v_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if (tr_on && it == tr_it && tr_cur == tr_s) tr_t[i] = v_;                               \
+  } while (0)
+#else
+#define A5_STAMP(i)
+#endif
   bool run = p < PW && bb + p < P.B && !(a.active && !a.active[bb + p]);
   const bool act = run;
   if (!__ballot(run)) return;
@@ -1271,14 +1290,20 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   // the step's vectors (rows ci of v0, cb of v1: the last stage's 12 rows clamped) and the first
   // two coefficient sets
   auto begin = [&](int s, int slot, int ci, int cb) {
+#ifdef I7M_DIAG
+    tr_cur = s;
+#endif
+    A5_STAMP(0);
     if constexpr (PW == 4)
       a5_wait();
     else
       a5_wait2();
+    A5_STAMP(1);
     int sn = s + 2, sl = slot + 2;
     if (sn >= 2 * N) sn -= 2 * N;
     if (sl >= 3) sl -= 3;
     issue(sn, sl, it > 1 || sn < s);
+    A5_STAMP(2);
     const double* S = ring + 2 * SLOT * slot;
     R = S + A5_LREC * (p < PW ? p : PL);
     const double* V = S + VD + 2 * A5_VP * (p < PW ? p : PL);  // [v0 18 | v1 18 | z 12 | y 12 | l 12 | I 12]
@@ -1292,15 +1317,20 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     ib1 = V[72 + cc];
     a4_ldj(CJ, R, c);
     a4_ldl(CL, R, R + a5_lrow(c), c);
+    A5_STAMP(3);
   };
   // store offsets: masked (past the range) for rows that do not run
   auto so = [&](bool ok, unsigned off) { return run && ok ? off + 0u : A5_OOB + 0u; };
   // Linv' Linv r, with J's row set read behind the first product when `jr`
   auto llt = [&](const A4Vec& r, bool jr) {
+    A5_STAMP(4);
     a4_ldt(CT, R, c);
     const A4Vec y = a4_lmul(CL, r);
+    A5_STAMP(5);
     if (jr) a4_ldr(CR, R, c);
-    return a4_ltmul(CL, CT, y);
+    const A4Vec o = a4_ltmul(CL, CT, y);
+    A5_STAMP(6);
+    return o;
   };
   // forward step k < N - 1: rhs, g, h = Linv' Linv g (stored), the next coupling J_k h
   auto fwd = [&](int k) {
@@ -1315,9 +1345,11 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const A4Vec h = llt(r, true);
     a5_st(h.lo, rA, so(true, hT + 8u * (18 * k + c)));
     a5_st(c == 0 ? h.h16 + 0.0 : h.h17 + 0.0, rA, so(lo2, hT + 8u * (18 * k + c16)));
+    A5_STAMP(7);
     hc.lo = a4_jmul(CR, c, h);
     tk = t1;
     ibk = ib1;
+    A5_STAMP(8);
   };
   // the last forward step (k = N - 1: 12 rows, no J, no u-part)
   auto fwd_last = [&]() {
@@ -1335,6 +1367,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const A4Vec s2 = llt(a4_jtmul(CJ, u, A4Vec{0.0, 0.0, 0.0}), true);
     const A4Vec xt{__dsub_rn(v0, s2.lo), __dsub_rn(hv0.x, s2.h16), __dsub_rn(hv0.y, s2.h17)};
     const double zt = __dadd_rn(a4_jmul(CR, c, xt), __dmul_rn(ib1, hc.lo));
+    A5_STAMP(7);
     const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z1));
     double zn = __dadd_rn(zr, __dmul_rn(ri, y1));
     zn = fmin(fmax(zn, l1), l1);
@@ -1355,6 +1388,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
       ny1 = yn;
     }
     hc = xt;
+    A5_STAMP(8);
   };
   // an iteration's 2N steps (ring slot `slot` = the step count mod 3): forward k = s < N - 1, the
   // last forward step (s = N - 1), the backward sweep's start (s = N: xt_{N-1} = h_{N-1}, already in
@@ -1485,6 +1519,14 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     const bool approx = exact ? false : test(10.0);
     st_v = solved ? 1 : (exact ? 1 : (approx ? 2 : 0));
   }
+#ifdef I7M_DIAG
+  if (tr_on && l == 0 && g_tl) {
+    unsigned long long* r = g_tl + 8 + 4 * (5ull << 16);
+    for (int i = 0; i < 9; ++i) r[i] = tr_t[i];
+    r[9] = (unsigned long long)a.ablate;
+  }
+#undef A5_STAMP
+#endif
   if (c == 0 && act) {
     a.srho[bown] = rho;
     if (a.iters) a.iters[(long)bown * 8 + a.sqp_iter] = solved ? done_it : a.A.max_iter;
@@ -1496,6 +1538,267 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
     double* so_ = a.sol + (long)bown * T;
     for (int e = c; e < T; e += 16) so_[e] = D[e] * xo[e];
   }
+}
+
+// ---- k_admm_iter_res: one problem per wave, everything it reads resident in LDS -------------
+// The streaming kernel's step issues 13 (or 7) LDS-DMA wave-instructions and 2-4 buffer stores,
+// and a lone wave's step is bound by their issue (tools/step_stamps.py: ~400 of ~1700 cycles for
+// the DMA, ~70 per store).  A launch of at most a CU's worth of problems has the LDS for a better
+// layout: one problem per workgroup, its N stage records (the streaming ring's image, 2.5 KB per
+// stage) and its vectors x, q, h, z, y, l, I (0.8 KB per stage) copied into LDS once, the sweeps
+// reading and writing LDS only (no DMA, no vector-memory wait in the loop), the vectors written
+// back before each termination test (which reads global memory) and at the end.  All four 16-lane
+// rows compute the problem (identical values to identical LDS addresses), so no lane is masked.
+// The same operations in the same order as admm_iter4 (bit-identical: its register patches for
+// data the ring loaded before the sweep wrote it read the same values from LDS here, except block
+// 1's z, which the ring takes from l's lines after the first iteration, as here).  Horizons up to
+// ARES_N (N = 32: 107 KB).
+constexpr int ARES_N = 32;
+__device__ __forceinline__ void a5_dma1(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned off) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(off), "s"(r)
+      : "memory");
+}
+template <int NR>
+__device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
+  const SolveParams& P = a.P;
+  const int N = P.N, T = P.T, m = 12 * N;
+  const int l = threadIdx.x, c = l & 15;
+  const int b = a.b0 + (int)blockIdx.x;
+  if (b >= P.B || (a.active && !a.active[b])) return;
+  __shared__ double2 sRec2[NR * A5_LREC / 2];
+  __shared__ double2 sV2[(3 * 18 + 4 * 12) * NR / 2 + 8];
+  double* const sRec = (double*)sRec2;
+  double* const sX = (double*)sV2;  // x | q | h (18 per stage) | z | y | l | I (12 per stage) | 16 spare
+  double* const sQ = sX + 18 * NR;
+  double* const sH = sQ + 18 * NR;
+  double* const sZ = sH + 18 * NR;
+  double* const sY = sZ + 12 * NR;
+  double* const sL = sY + 12 * NR;
+  double* const sI = sL + 12 * NR;
+  double* const sJunk = sI + 12 * NR;  // stores of lanes that have none
+  auto lds = [](const void* q) { return (unsigned)(unsigned long)(__attribute__((address_space(3))) const void*)q; };
+  const auto rA = a4_rsrc(a.abase, a.abytes);
+  auto boff = [&](const double* q) { return (unsigned)__builtin_amdgcn_readfirstlane((int)((const char*)q - (const char*)a.abase)); };
+  const unsigned oX = boff(a.sx + (long)b * T), oQ = boff(a.qs + (long)b * T), oZ = boff(a.sz + (long)b * m);
+  const unsigned oY = boff(a.sy + (long)b * m), oL = boff(a.ls + (long)b * m), oI = boff(a.I + (long)b * m);
+  const unsigned oR = boff(a.R + (long)b * N * ADM_REC);
+  // the stage records, in the ring's image (piece j of a stage from its HBM piece, zeros past a
+  // row's stored width), and the vectors; the stage-N-1 tails of x and q (never used) zeroed
+  {
+    const int np = N * A5_RP;
+    for (int g0 = 0; g0 < np; g0 += 64) {
+      const int g = g0 + l, k = g / A5_RP, j = g - A5_RP * k;
+      int hp;
+      if (j < 80) {
+        int r = 0;
+#pragma unroll
+        for (int i = 1; i < 16; ++i) r = 2 * j >= a5_lrow(i) ? i : r;
+        const int cp = 2 * j - a5_lrow(r);
+        hp = cp < adm_lw(r) ? (adm_lrow(r) + cp) / 2 : -1;
+      } else {
+        hp = j - 8;
+      }
+      a5_dma1(rA, lds(sRec) + 16u * g0, g < np && hp >= 0 ? oR + 8u * (unsigned)(k * ADM_REC) + 16u * hp : A5_OOB);
+    }
+    auto copy = [&](double* dst, unsigned src, int n) {  // n doubles (even)
+      for (int g0 = 0; g0 < n / 2; g0 += 64) a5_dma1(rA, lds(dst) + 16u * g0, g0 + l < n / 2 ? src + 16u * (g0 + l) : A5_OOB);
+    };
+    copy(sX, oX, T);
+    copy(sQ, oQ, T);
+    copy(sZ, oZ, m);
+    copy(sY, oY, m);
+    copy(sL, oL, m);
+    copy(sI, oI, m);
+    if (l < 6) {
+      sX[T + l] = 0.0;
+      sQ[T + l] = 0.0;
+    }
+    a5_drain();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  // the vectors the termination test reads, back to global memory (every lane a different entry)
+  auto flush = [&]() {
+    for (int e = l; e < T; e += 64) a5_st(sX[e], rA, oX + 8u * e);
+    for (int e = l; e < m; e += 64) {
+      a5_st(sZ[e], rA, oZ + 8u * e);
+      a5_st(sY[e], rA, oY + 8u * e);
+    }
+    a5_drain();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  const double c_cost = a.cs[b];
+  const double rho = a.srho[b], rv = 1e3 * rho, ri = 1.0 / rv;
+  const double al = a.A.alpha, sg = a.A.sigma, al1 = 1.0 - al;
+  const int cc = c < 12 ? c : 11;
+  const bool lo12 = c < 12, lo2 = c < 2;
+  double* const junk = sJunk + c;
+  int it = 1;
+  A4Vec hc{0.0, 0.0, 0.0};
+  double b0z = sZ[cc], b0y = sY[cc], b0l = sL[cc], b0i = sI[cc];
+  double nz1 = 0.0;
+  // x_0 rides in registers from epilogue to epilogue, as in admm_iter4 (the same value as sX, but
+  // the compiler's fusing of the epilogue's products into its sum follows where the operand comes
+  // from: read from LDS there, x_0's update rounded differently in the last place)
+  double nx0 = sX[c];
+  double2 nx0h = make_double2(sX[16], sX[17]);
+  double tk = __dmul_rn(rv, __dsub_rn(b0z, __dmul_rn(ri, b0y)));
+  double ibk = b0i;
+  int done_it = 0;
+  bool solved = false;
+  double v0, v1, z1, y1, l1, ib1;
+  double2 hv0, hv1;
+  A4CJ CJ;
+  A4CL CL;
+  A4CT CT;
+  A4CR CR;
+  const double* R = nullptr;
+  // a step's operands: stage k's record, v0 / v1 (rows ci / cb) from the given vectors, block
+  // k1's rows (z from l's lines after the first iteration), the first two coefficient sets
+  auto begin = [&](int k, const double* V0, const double* V1, int k1, int ci, int cb) {
+    R = sRec + A5_LREC * k;
+    v0 = V0[ci];
+    v1 = V1[cb];
+    hv0 = make_double2(V0[16], V0[17]);
+    hv1 = make_double2(V1[16], V1[17]);
+    z1 = (it > 1 ? sL : sZ)[12 * k1 + cc];
+    y1 = sY[12 * k1 + cc];
+    l1 = sL[12 * k1 + cc];
+    ib1 = sI[12 * k1 + cc];
+    a4_ldj(CJ, R, c);
+    a4_ldl(CL, R, R + a5_lrow(c), c);
+  };
+  auto llt = [&](const A4Vec& r, bool jr) {
+    a4_ldt(CT, R, c);
+    const A4Vec y = a4_lmul(CL, r);
+    if (jr) a4_ldr(CR, R, c);
+    return a4_ltmul(CL, CT, y);
+  };
+  for (; it <= a.A.max_iter; ++it) {
+    // forward steps k < N - 1
+    for (int k = 0; k < N - 1; ++k) {
+      begin(k, sX + 18 * k, sQ + 18 * k, k + 1, c, c);
+      if (it > 1 && k == 0) z1 = nz1;
+      const double t1 = __dmul_rn(rv, __dsub_rn(z1, __dmul_rn(ri, y1)));
+      const double init = lo12 ? __dmul_rn(ibk, tk) : 0.0;
+      A4Vec r = a4_jtmul(CJ, t1, A4Vec{init, 0.0, 0.0});
+      r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
+      r.h16 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.x), hv1.x), r.h16);
+      r.h17 = __dadd_rn(__dsub_rn(__dmul_rn(sg, hv0.y), hv1.y), r.h17);
+      const double rc = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));
+      r.lo = lo12 ? rc : r.lo;
+      const A4Vec h = llt(r, true);
+      double* const H = sH + 18 * k;
+      H[c] = h.lo;
+      *(lo2 ? H + 16 + c : junk) = c == 0 ? h.h16 : h.h17;
+      hc.lo = a4_jmul(CR, c, h);
+      tk = t1;
+      ibk = ib1;
+    }
+    // the last forward step (12 rows, no J, no u-part): xt_{N-1} = h_{N-1}, kept in registers
+    {
+      const int k = N - 1;
+      begin(k, sX + 18 * k, sQ + 18 * k, k, cc, cc);
+      A4Vec r{lo12 ? __dmul_rn(ibk, tk) : 0.0, 0.0, 0.0};
+      r.lo = __dadd_rn(__dsub_rn(__dmul_rn(sg, v0), v1), r.lo);
+      r.lo = __dsub_rn(r.lo, __dmul_rn(__dmul_rn(rv, ibk), hc.lo));
+      r.lo = lo12 ? r.lo : 0.0;
+      hc = llt(r, false);
+    }
+    // backward steps k = N - 2 .. 0: xt_k, then block k+1's rows and x_{k+1}
+    for (int k = N - 2; k >= 0; --k) {
+      const bool last1 = k + 1 == N - 1;  // x_{k+1} has no u-part
+      begin(k, sH + 18 * k, sX + 18 * (k + 1), k + 1, c, last1 ? cc : c);
+      const double u = __dmul_rn(__dmul_rn(rv, ib1), hc.lo);
+      const A4Vec s2 = llt(a4_jtmul(CJ, u, A4Vec{0.0, 0.0, 0.0}), true);
+      const A4Vec xt{__dsub_rn(v0, s2.lo), __dsub_rn(hv0.x, s2.h16), __dsub_rn(hv0.y, s2.h17)};
+      const double zt = __dadd_rn(a4_jmul(CR, c, xt), __dmul_rn(ib1, hc.lo));
+      const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z1));
+      double zn = __dadd_rn(zr, __dmul_rn(ri, y1));
+      zn = fmin(fmax(zn, l1), l1);
+      const double yn = __dadd_rn(y1, __dmul_rn(rv, __dsub_rn(zr, zn)));
+      const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, v1));
+      const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, hv1.x));
+      const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, hv1.y));
+      const int ob = 12 * (k + 1);
+      *(lo12 && it == 1 ? sZ + ob + c : junk) = zn;
+      *(lo12 ? sY + ob + c : junk) = yn;
+      double* const X1 = sX + 18 * (k + 1);
+      *(!last1 || lo12 ? X1 + c : junk) = xn;
+      *(!last1 && lo2 ? X1 + 16 + c : junk) = c == 0 ? xn16 : xn17;
+      if (k == 0) nz1 = zn;
+      hc = xt;
+    }
+    // block 0's rows (z~ = I xt_0) and x_0
+    {
+      const double x0 = nx0, x016 = nx0h.x, x017 = nx0h.y;
+      const double zt = __dmul_rn(b0i, hc.lo);
+      const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, b0z));
+      double zn = __dadd_rn(zr, __dmul_rn(ri, b0y));
+      zn = fmin(fmax(zn, b0l), b0l);
+      const double yn = __dadd_rn(b0y, __dmul_rn(rv, __dsub_rn(zr, zn)));
+      const double xn = __dadd_rn(__dmul_rn(al, hc.lo), __dmul_rn(al1, x0));
+      const double xn16 = __dadd_rn(__dmul_rn(al, hc.h16), __dmul_rn(al1, x016));
+      const double xn17 = __dadd_rn(__dmul_rn(al, hc.h17), __dmul_rn(al1, x017));
+      *(lo12 && it == 1 ? sZ + c : junk) = zn;
+      *(lo12 ? sY + c : junk) = yn;
+      sX[c] = xn;
+      *(lo2 ? sX + 16 + c : junk) = c == 0 ? xn16 : xn17;
+      nx0 = xn;
+      nx0h = make_double2(xn16, xn17);
+      b0z = zn;
+      b0y = yn;
+      tk = __dmul_rn(rv, __dsub_rn(zn, __dmul_rn(ri, yn)));
+      ibk = b0i;
+      hc = A4Vec{0.0, 0.0, 0.0};
+    }
+    if (a.A.check && it % a.A.check == 0) {
+      flush();
+      double rest = rho;
+      const bool ok = adm_check<16>(a, N, T, m, c_cost, rho, a.sx + (long)b * T, a.sz + (long)b * m, a.sy + (long)b * m,
+                                    a.qs + (long)b * T, a.ls + (long)b * m, a.D + (long)b * T, a.E + (long)b * m,
+                                    a.R + (long)b * N * ADM_REC + REC_J, a.I + (long)b * m, a.Pq + (long)b * N * 36,
+                                    a.Pd + (long)b * T, &rest, c);
+      if (ok) {
+        solved = true;
+        done_it = it;
+        break;
+      }
+    }
+  }
+  if (!solved) flush();
+  // OSQP's closing tests after max_iter (as admm_iter4)
+  int st_v = solved ? 1 : 0;
+  if (!solved) {
+    auto test = [&](double es) {
+      double rest = rho;
+      return adm_check<16>(a, N, T, m, c_cost, rho, a.sx + (long)b * T, a.sz + (long)b * m, a.sy + (long)b * m,
+                           a.qs + (long)b * T, a.ls + (long)b * m, a.D + (long)b * T, a.E + (long)b * m,
+                           a.R + (long)b * N * ADM_REC + REC_J, a.I + (long)b * m, a.Pq + (long)b * N * 36,
+                           a.Pd + (long)b * T, &rest, c, es);
+    };
+    const bool last_checked = a.A.check && a.A.max_iter % a.A.check == 0;
+    const bool exact = last_checked ? false : test(1.0);
+    const bool approx = exact ? false : test(10.0);
+    st_v = exact ? 1 : (approx ? 2 : 0);
+  }
+  if (l == 0) {
+    a.srho[b] = rho;
+    if (a.iters) a.iters[(long)b * 8 + a.sqp_iter] = solved ? done_it : a.A.max_iter;
+    if (a.status) a.status[(long)b * 8 + a.sqp_iter] = st_v;
+  }
+  const double* D = a.D + (long)b * T;
+  double* so_ = a.sol + (long)b * T;
+  for (int e = l; e < T; e += 64) so_[e] = D[e] * sX[e];
 }
 
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
@@ -1518,6 +1821,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 // at B = 4096 the doubled instruction count per problem costs more than the second wave hides
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_admm_iter2(AdmmArgs a) {
   admm_iter4<false, 2>(a);
+}
+// one problem per workgroup, records and vectors resident in LDS (grid = problems; N <= ARES_N)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter_res(AdmmArgs a) {
+  admm_iter_res<ARES_N>(a);
 }
 
 }  // namespace i7m

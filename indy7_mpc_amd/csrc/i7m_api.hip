@@ -152,6 +152,11 @@ struct i7m_handle {
   // B <= 256, level at 1 024, 19-32 % longer at 4 096 (profiles/r06p, r06q); I7M_ADMM_ITER2 = 0
   // never, 1 always, -1 (default) by that size
   int admm_iter2 = -1;
+  // k_admm_iter_res (one problem per workgroup, its records and vectors resident in LDS) for
+  // launches of at most admm_res_max problems at N <= ARES_N without rho adaptation; I7M_ADMM_RES
+  // = 0 never, 1 whenever it fits, -1 (default) by that size
+  int admm_res = -1;
+  int admm_res_max = 256;
   int admm_chains = 1;  // ranges r wait for range r - chains's mark (I7M_ADMM_CHAINS, A/B: 2 = two independent stagger chains)
   int admm_split = 500;  // two ranges: the first's share of the batch, per mille (I7M_ADMM_SPLIT, A/B)
   int admm_stagger_min_b = 3072;  // measured, two ranges: B = 8192 / 4096 / 3072 +9 / +17 / +5 %; 2048 / 1024 -8 / -11 %
@@ -573,8 +578,11 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
         AdmmArgs a4 = a;
         a4.P = P4;
         const dim3 g((n + 3) / 4);
+        const bool res_fits = !a.A.adapt_interval && a.P.N <= ARES_N;
         if (a.A.adapt_interval)
           hipExtLaunchKernelGGL(k_admm_iter<true>, g, dim3(64), 0, s, ea, eb, 0, a4);
+        else if (res_fits && (h->admm_res > 0 || (h->admm_res < 0 && n <= h->admm_res_max)))
+          hipExtLaunchKernelGGL(k_admm_iter_res, dim3(n), dim3(64), 0, s, ea, eb, 0, a4);
         else if (h->admm_iter2 > 0 || (h->admm_iter2 < 0 && n <= 512))  // two problems per wave
           hipExtLaunchKernelGGL(k_admm_iter2, dim3((n + 1) / 2), dim3(64), 0, s, ea, eb, 0, a4);
         else
@@ -1132,6 +1140,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
     h->admm_ranges = std::min(std::max(std::atoi(e), 1), (int)i7m_handle::kMaxRanges);
   if (const char* e = std::getenv("I7M_ADMM_CHAINS")) h->admm_chains = std::min(std::max(std::atoi(e), 1), 2);
   if (const char* e = std::getenv("I7M_ADMM_ITER2")) h->admm_iter2 = std::min(std::max(std::atoi(e), -1), 1);
+  if (const char* e = std::getenv("I7M_ADMM_RES")) h->admm_res = std::min(std::max(std::atoi(e), -1), 1);
+  if (const char* e = std::getenv("I7M_ADMM_RES_MAX")) h->admm_res_max = std::max(std::atoi(e), 0);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||

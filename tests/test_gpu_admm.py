@@ -370,21 +370,30 @@ def test_admm_status_after_max_iter_matches_port(lib, model, max_iter, eps):
         QPSolution.from_admm(None, -1, 0, None)
 
 
-@pytest.mark.parametrize("B", [13, 600])
-def test_admm_iter_two_and_four_problems_per_wave_bit_identical(lib, model, monkeypatch, B):
-    """k_admm_iter2 (two problems per wave, used for launches of <= 512 problems) and k_admm_iter
-    (four) run the same arithmetic per problem: two consecutive solves with each forced
-    (I7M_ADMM_ITER2 = 1 / 0) are equal bit for bit, carried state, OSQP records and statuses
-    included (B = 13: empty rows in the last wave of both)."""
-    N = 32
+KERNELS = (("res", {"I7M_ADMM_RES": "1", "I7M_ADMM_ITER2": "-1"}),
+           ("iter2", {"I7M_ADMM_RES": "0", "I7M_ADMM_ITER2": "1"}),
+           ("iter4", {"I7M_ADMM_RES": "0", "I7M_ADMM_ITER2": "0"}))
+
+
+@pytest.mark.parametrize("B,N,admm", [(13, 32, None), (600, 32, None), (1, 32, None), (13, 16, None),
+                                      (13, 32, {"max_iter": 20})])
+def test_admm_iteration_kernels_bit_identical(lib, model, monkeypatch, B, N, admm):
+    """The three OSQP iteration kernels run the same arithmetic per problem: k_admm_iter_res (one
+    problem per workgroup, LDS-resident: launches of <= 256 problems at N <= 32), k_admm_iter2 (two
+    per wave: <= 512) and k_admm_iter (four), each forced (I7M_ADMM_RES, I7M_ADMM_ITER2): two
+    consecutive solves are equal bit for bit, carried state, OSQP records and statuses included
+    (B = 13: empty rows in the streaming kernels' last wave; max_iter 20: the closing tests)."""
     xcur, goals, XU = synthetic_batch(B, N, 54)
     res = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("I7M_ADMM_ITER2", mode)
-        h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM)
+    for _, env in KERNELS:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        kw = {"admm": admm} if admm else {}
+        h = lib.Handle(model, N=N, max_batch=B, qp_mode=lib.QP_ADMM, **kw)
         o1, _ = h.solve(xcur, goals, XU)
         o2, _ = h.solve(xcur, goals, o1)
         res.append((o1, o2) + h.admm_state(B) + h.admm_stats(B, with_status=True))
         h.close()
-    for a, b in zip(*res):
-        np.testing.assert_array_equal(a, b)
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            np.testing.assert_array_equal(a, b)
