@@ -1664,7 +1664,29 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
   const double* R = nullptr;
   // a step's operands: stage k's record, v0 / v1 (rows ci / cb) from the given vectors, block
   // k1's rows (z from l's lines after the first iteration), the first two coefficient sets
+#ifdef I7M_DIAG
+  // the step stamps of admm_iter4 (I7M_ABLATE 100000 + 100 IT + S; tools/step_stamps.py --res):
+  // step start, its reads issued, right-hand side, Linv r, Linv' y, stores, end
+  const int tr_it = a.ablate >= 100000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
+  const bool tr_on = tr_it >= 0 && blockIdx.x == 0;
+  unsigned long long tr_t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int tr_cur = -1;
+#define AR_STAMP(i)                                                                         \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long v_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if (tr_on && it == tr_it && tr_cur == tr_s) tr_t[i] = v_;                               \
+  } while (0)
+#else
+#define AR_STAMP(i)
+#endif
   auto begin = [&](int k, const double* V0, const double* V1, int k1, int ci, int cb) {
+#ifdef I7M_DIAG
+    tr_cur = k1 == k + 1 && V0 == sH + 18 * k ? 2 * N - 1 - k : k;
+#endif
+    AR_STAMP(0);
     R = sRec + A5_LREC * k;
     v0 = V0[ci];
     v1 = V1[cb];
@@ -1676,12 +1698,17 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
     ib1 = sI[12 * k1 + cc];
     a4_ldj(CJ, R, c);
     a4_ldl(CL, R, R + a5_lrow(c), c);
+    AR_STAMP(1);
   };
   auto llt = [&](const A4Vec& r, bool jr) {
+    AR_STAMP(2);
     a4_ldt(CT, R, c);
     const A4Vec y = a4_lmul(CL, r);
+    AR_STAMP(3);
     if (jr) a4_ldr(CR, R, c);
-    return a4_ltmul(CL, CT, y);
+    const A4Vec o = a4_ltmul(CL, CT, y);
+    AR_STAMP(4);
+    return o;
   };
   for (; it <= a.A.max_iter; ++it) {
     // forward steps k < N - 1
@@ -1700,9 +1727,11 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
       double* const H = sH + 18 * k;
       H[c] = h.lo;
       *(lo2 ? H + 16 + c : junk) = c == 0 ? h.h16 : h.h17;
+      AR_STAMP(5);
       hc.lo = a4_jmul(CR, c, h);
       tk = t1;
       ibk = ib1;
+      AR_STAMP(6);
     }
     // the last forward step (12 rows, no J, no u-part): xt_{N-1} = h_{N-1}, kept in registers
     {
@@ -1722,6 +1751,7 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
       const A4Vec s2 = llt(a4_jtmul(CJ, u, A4Vec{0.0, 0.0, 0.0}), true);
       const A4Vec xt{__dsub_rn(v0, s2.lo), __dsub_rn(hv0.x, s2.h16), __dsub_rn(hv0.y, s2.h17)};
       const double zt = __dadd_rn(a4_jmul(CR, c, xt), __dmul_rn(ib1, hc.lo));
+      AR_STAMP(5);
       const double zr = __dadd_rn(__dmul_rn(al, zt), __dmul_rn(al1, z1));
       double zn = __dadd_rn(zr, __dmul_rn(ri, y1));
       zn = fmin(fmax(zn, l1), l1);
@@ -1737,6 +1767,7 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
       *(!last1 && lo2 ? X1 + 16 + c : junk) = c == 0 ? xn16 : xn17;
       if (k == 0) nz1 = zn;
       hc = xt;
+      AR_STAMP(6);
     }
     // block 0's rows (z~ = I xt_0) and x_0
     {
@@ -1791,6 +1822,15 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
     const bool approx = exact ? false : test(10.0);
     st_v = exact ? 1 : (approx ? 2 : 0);
   }
+#ifdef I7M_DIAG
+  if (tr_on && l == 0 && g_tl) {
+    unsigned long long* r = g_tl + 8 + 4 * (5ull << 16);
+    for (int i = 0; i < 9; ++i) r[i] = tr_t[i];
+    r[9] = (unsigned long long)a.ablate;
+    r[10] = 1;  // the resident kernel's stamp layout
+  }
+#undef AR_STAMP
+#endif
   if (l == 0) {
     a.srho[b] = rho;
     if (a.iters) a.iters[(long)b * 8 + a.sqp_iter] = solved ? done_it : a.A.max_iter;

@@ -16,6 +16,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SEG = ["wait", "dma", "lds", "pre", "lmul", "ltmul", "st", "jmul"]
+# k_admm_iter_res (launches of <= 256 problems): no ring, so no wait or DMA segment; its fifth and
+# sixth segments are the stores then J h (forward) or J xt then the rows' update and stores (backward)
+SEG_RES = ["lds", "pre", "lmul", "ltmul", "st|jmul", "jmul|upd+st"]
 
 
 def main():
@@ -56,12 +59,14 @@ def main():
             h.solve_device(a.B, t_xu.data_ptr(), t_xs.data_ptr(), t_g.data_ptr(), 3, t_out.data_ptr(), None)
             torch.cuda.synchronize(dev)
             lib.i7m_diag_timeline(C.c_void_p(0))
-        t = buf[base:base + 10].cpu().tolist()
+        t = buf[base:base + 11].cpu().tolist()
         h.close()
-        d = [t[i + 1] - t[i] if t[i + 1] and t[i] else None for i in range(8)]
+        res = t[10] == 1
+        ns = 6 if res else 8
+        d = [t[i + 1] - t[i] if t[i + 1] and t[i] else None for i in range(ns)]
         kind = "fwd" if S < a.N - 1 else ("fwd_last" if S == a.N - 1 else ("turn" if S == a.N else "bwd"))
-        r = {"B": a.B, "it": a.it, "step": S, "kind": kind, "tag": t[9], "cycles": dict(zip(SEG, d)),
-             "total": (t[8] - t[0]) if t[8] and t[0] else None}
+        r = {"B": a.B, "it": a.it, "step": S, "kind": kind, "tag": t[9], "kernel": "res" if res else "streaming",
+             "cycles": dict(zip(SEG_RES if res else SEG, d)), "total": (t[ns] - t[0]) if t[ns] and t[0] else None}
         rows.append(r)
         print(json.dumps(r), flush=True)
 
