@@ -634,7 +634,25 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
         : "memory");
   };
   fetch(0);
+#ifdef I7M_DIAG
+  // I7M_ABLATE 200000 + K (tools/step_stamps.py --factor): s_memtime at the phases of stage K of
+  // workgroup 0's factor (its own launch: the record area 5 of the timeline buffer)
+  const int fs_k = a.ablate >= 200000 ? a.ablate - 200000 : -1;
+  const bool fs_on = fs_k >= 0 && blockIdx.x == 0;
+  unsigned long long fs_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define AF_STAMP(i)                                                                         \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long v_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if (fs_on && k == fs_k) fs_t[i] = v_;                                                   \
+  } while (0)
+#else
+#define AF_STAMP(i)
+#endif
   for (int k = 0; k < N; ++k) {
+    AF_STAMP(0);
     const int nk = k < N - 1 ? 18 : 12;
     // every stage recomputes the lane's indices (hoisted out of the stage loop they would take
     // more registers than the kernel has)
@@ -646,6 +664,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     const double* G = stg + AF_STG * (k & 1);
     if (k < N - 1) adm_stage_J(sJ, G, l);
     wave_sync();
+    AF_STAMP(1);
     // S is symmetric to the bit (every term's products commute and sum in the same order), so the
     // lanes form its lower triangle (171 entries) and mirror it
 #pragma unroll
@@ -671,6 +690,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       }
     }
     wave_sync();
+    AF_STAMP(2);
     double r[18];
 #pragma unroll
     for (int j = 0; j < 18; ++j) r[j] = sS[FS * lr + j];
@@ -690,6 +710,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
         for (int j = p + 1; j < 18; ++j) r[j] = r[j] - r[p] * col[j];
       }
     }
+    AF_STAMP(3);
     wave_sync();  // every lane has read S before L overwrites it
     static_assert(FS >= 19, "the row's spare column holds 1 / L_ii");
     if (l < 18) {
@@ -698,6 +719,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       sS[FS * l + 18] = myid;
     }
     wave_sync();
+    AF_STAMP(4);
     double x[18];
 #pragma unroll
     for (int i = 0; i < 18; ++i) {
@@ -718,6 +740,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
       }
     }
     wave_sync();
+    AF_STAMP(5);
     if (k < N - 1) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -733,7 +756,17 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
     // (LDS only: the stage's global stores are read by no later stage, and the kernel's end or the
     // re-factoring caller's fence orders them; a global release here waited for them every stage)
     wave_sync_fence();
+    AF_STAMP(6);
   }
+#ifdef I7M_DIAG
+  if (fs_on && l0 == 0 && g_tl) {
+    unsigned long long* r = g_tl + 8 + 4 * (5ull << 16);
+    for (int i = 0; i < 7; ++i) r[i] = fs_t[i];
+    r[9] = (unsigned long long)a.ablate;
+    r[10] = 2;  // the factor's stamp layout
+  }
+#undef AF_STAMP
+#endif
 }
 
 // The factor with every step's operands through LDS (the kernel before the register Cholesky;
@@ -1143,7 +1176,7 @@ __device__ __forceinline__ void admm_iter4(const AdmmArgs& a) {
   // I7M_ABLATE 100000 + 100 IT + S (tools/step_stamps.py): s_memtime (shader cycles) at nine points
   // of sweep step S of OSQP iteration IT in workgroup 0, to the timeline buffer's record area 5
   // (stamps fenced by sched barriers: read the shares, not the length)
-  const int tr_it = a.ablate >= 100000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
+  const int tr_it = a.ablate >= 100000 && a.ablate < 200000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
   const bool tr_on = tr_it >= 0 && blockIdx.x == 0;
   unsigned long long tr_t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int tr_cur = -1;
@@ -1667,7 +1700,7 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
 #ifdef I7M_DIAG
   // the step stamps of admm_iter4 (I7M_ABLATE 100000 + 100 IT + S; tools/step_stamps.py --res):
   // step start, its reads issued, right-hand side, Linv r, Linv' y, stores, end
-  const int tr_it = a.ablate >= 100000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
+  const int tr_it = a.ablate >= 100000 && a.ablate < 200000 ? (a.ablate - 100000) / 100 : -1, tr_s = a.ablate % 100;
   const bool tr_on = tr_it >= 0 && blockIdx.x == 0;
   unsigned long long tr_t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int tr_cur = -1;

@@ -157,6 +157,9 @@ struct i7m_handle {
   // = 0 never, 1 whenever it fits, -1 (default) by that size
   int admm_res = -1;
   int admm_res_max = 256;
+  // extra dynamic LDS per k_admm_iter workgroup (I7M_ADMM_ITER_DYN_LDS, bytes; A/B): past 160 KB / 4
+  // it leaves one SIMD of every CU, and its LDS, to the other range's kernels
+  int admm_iter_dyn_lds = 0;
   int admm_chains = 1;  // ranges r wait for range r - chains's mark (I7M_ADMM_CHAINS, A/B: 2 = two independent stagger chains)
   int admm_split = 500;  // two ranges: the first's share of the batch, per mille (I7M_ADMM_SPLIT, A/B)
   int admm_stagger_min_b = 3072;  // measured, two ranges: B = 8192 / 4096 / 3072 +9 / +17 / +5 %; 2048 / 1024 -8 / -11 %
@@ -586,7 +589,7 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
         else if (h->admm_iter2 > 0 || (h->admm_iter2 < 0 && n <= 512))  // two problems per wave
           hipExtLaunchKernelGGL(k_admm_iter2, dim3((n + 1) / 2), dim3(64), 0, s, ea, eb, 0, a4);
         else
-          hipExtLaunchKernelGGL(k_admm_iter<false>, g, dim3(64), 0, s, ea, eb, 0, a4);
+          hipExtLaunchKernelGGL(k_admm_iter<false>, g, dim3(64), h->admm_iter_dyn_lds, s, ea, eb, 0, a4);
       });
       if (rc2) return rc2;
     }
@@ -1142,6 +1145,7 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_ADMM_ITER2")) h->admm_iter2 = std::min(std::max(std::atoi(e), -1), 1);
   if (const char* e = std::getenv("I7M_ADMM_RES")) h->admm_res = std::min(std::max(std::atoi(e), -1), 1);
   if (const char* e = std::getenv("I7M_ADMM_RES_MAX")) h->admm_res_max = std::max(std::atoi(e), 0);
+  if (const char* e = std::getenv("I7M_ADMM_ITER_DYN_LDS")) h->admm_iter_dyn_lds = std::min(std::max(std::atoi(e), 0), 65536);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->cs[1], hipStreamNonBlocking) != hipSuccess ||
