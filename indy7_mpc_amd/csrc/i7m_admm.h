@@ -402,7 +402,25 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
         av[r][j] = sv ? L[jb + 6 * (3 * hs + r)] : 0.0;  // (signed: the J output below uses it too)
       }
   }
+#ifdef I7M_DIAG
+  // I7M_ABLATE 300000 + P (tools/step_stamps.py --scale): s_memtime at the parts of Ruiz pass P of
+  // workgroup 0 (record area 5 of the timeline buffer)
+  const int ss_p = a.ablate >= 300000 ? a.ablate - 300000 : -1;
+  const bool ss_on = ss_p >= 0 && blockIdx.x == 0;
+  unsigned long long ss_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define AS_STAMP(i)                                                                         \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long v_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v_)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if (ss_on && pass == ss_p) ss_t[i] = v_;                                                \
+  } while (0)
+#else
+#define AS_STAMP(i)
+#endif
   for (int pass = 0; pass < a.A.scaling; ++pass) {
+    AS_STAMP(0);
     // every pass recomputes its indices (hoisted out of the pass loop they would take ~300 VGPRs)
     const double* Lp = LIN;
     const double* Cp = CO;
@@ -439,6 +457,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       }
       wave_sync_fence();
     }
+    AS_STAMP(1);
 #pragma unroll 3
     for (int t = 0; t < CT; ++t) {
       const int e = min(lp + 64 * t, T - 1), k = e / 18, j = e - 18 * k;
@@ -465,6 +484,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       if constexpr (REG) dtv[t] = 1.0 / sqrt(adm_limit(mx));
       else sDt[lp + 64 * t] = 1.0 / sqrt(adm_limit(mx));
     }
+    AS_STAMP(2);
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
       const int r = min(lp + 64 * t, m - 1), blk = r / 12, i = r - 12 * blk;
@@ -492,6 +512,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
       if (blk > 0) mx = fmax(mx, mj);
       etv[t] = 1.0 / sqrt(adm_limit(mx));
     }
+    AS_STAMP(3);
     wave_sync_fence();
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -506,6 +527,7 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
     for (int t = 0; t < RT; ++t)
       if (lp + 64 * t < m) sE[lp + 64 * t] = sE[lp + 64 * t] * etv[t];
     wave_sync_fence();
+    AS_STAMP(4);
     // cost normalisation: mean column norm of the scaled P, |q|
     double sm = 0.0, qm = 0.0;
 #pragma unroll
@@ -523,7 +545,18 @@ __device__ __forceinline__ double adm_scale(const AdmmArgs& a, int b, int N, int
 #pragma unroll
     for (int t = 0; t < CT; ++t) qv[t] = qv[t] * ct;
     c = c * ct;
+    AS_STAMP(5);
   }
+#ifdef I7M_DIAG
+  if (ss_on && l == 0 && g_tl) {
+    unsigned long long* r = g_tl + 8 + 4 * (5ull << 16);
+    for (int i = 0; i < 6; ++i) r[i] = ss_t[i];
+    r[6] = 0;
+    r[9] = (unsigned long long)a.ablate;
+    r[10] = 3;  // the scaling's stamp layout
+  }
+#undef AS_STAMP
+#endif
   // scaled data: P <- c D P D, J <- E J D, I <- -E D, q <- c D g (update(q)), l <- E l
   for (int e = l; e < T; e += 64) D[e] = sD[e];
   for (int r = l; r < m; r += 64) E[r] = sE[r];
@@ -637,7 +670,7 @@ __device__ __forceinline__ void adm_factor(const AdmmArgs& a, int N, double rho,
 #ifdef I7M_DIAG
   // I7M_ABLATE 200000 + K (tools/step_stamps.py --factor): s_memtime at the phases of stage K of
   // workgroup 0's factor (its own launch: the record area 5 of the timeline buffer)
-  const int fs_k = a.ablate >= 200000 ? a.ablate - 200000 : -1;
+  const int fs_k = a.ablate >= 200000 && a.ablate < 300000 ? a.ablate - 200000 : -1;
   const bool fs_on = fs_k >= 0 && blockIdx.x == 0;
   unsigned long long fs_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define AF_STAMP(i)                                                                         \

@@ -22,6 +22,9 @@ SEG_RES = ["lds", "pre", "lmul", "ltmul", "st|jmul", "jmul|upd+st"]
 # k_admm_factor (--factor: stage S of workgroup 0): the stage's operands and J staged, S formed,
 # the Cholesky, L written back, the inverse and the record stored, C_k
 SEG_FAC = ["wait+J", "S", "chol", "Lwrite", "inv+store", "Ck"]
+# k_admm_scale (--scale: Ruiz pass S of workgroup 0): the stage owners' v-row maxima, the column
+# norms, the row norms, D / E / q updated, the cost normalisation
+SEG_SCL = ["reg", "cols", "rows", "update", "cost"]
 
 
 def main():
@@ -31,6 +34,7 @@ def main():
     ap.add_argument("--it", type=int, default=3)
     ap.add_argument("--steps", default="1,2,5,10,20,30,31,33,34,35,40,50,60,63")
     ap.add_argument("--factor", action="store_true", help="stamp the factor's stage S instead of a sweep step")
+    ap.add_argument("--scale", action="store_true", help="stamp the scaling's Ruiz pass S instead of a sweep step")
     a = ap.parse_args()
     import torch
     from indy7_mpc_amd import _lib
@@ -49,7 +53,7 @@ def main():
     base = 8 + 4 * (5 << 16)
     rows = []
     for S in [int(x) for x in a.steps.split(",")]:
-        os.environ["I7M_ABLATE"] = str(200000 + S if a.factor else 100000 + 100 * a.it + S)
+        os.environ["I7M_ABLATE"] = str(300000 + S if a.scale else (200000 + S if a.factor else 100000 + 100 * a.it + S))
         h = _lib.Handle(model, N=a.N, max_batch=a.B, max_sqp_iters=1, qp_mode=_lib.QP_ADMM)
         os.environ.pop("I7M_ABLATE")
         xcur, goals, XU = make_batch(h, model, a.B, a.N, seed=44)
@@ -65,15 +69,15 @@ def main():
             lib.i7m_diag_timeline(C.c_void_p(0))
         t = buf[base:base + 11].cpu().tolist()
         h.close()
-        res, fac = t[10] == 1, t[10] == 2
-        ns = 6 if (res or fac) else 8
+        res, fac, scl = t[10] == 1, t[10] == 2, t[10] == 3
+        ns = 5 if scl else (6 if (res or fac) else 8)
         d = [t[i + 1] - t[i] if t[i + 1] and t[i] else None for i in range(ns)]
         kind = "fwd" if S < a.N - 1 else ("fwd_last" if S == a.N - 1 else ("turn" if S == a.N else "bwd"))
-        if fac:
-            kind = "factor stage"
+        if fac or scl:
+            kind = "factor stage" if fac else "Ruiz pass"
         r = {"B": a.B, "it": a.it, "step": S, "kind": kind, "tag": t[9],
-             "kernel": "factor" if fac else ("res" if res else "streaming"),
-             "cycles": dict(zip(SEG_FAC if fac else (SEG_RES if res else SEG), d)),
+             "kernel": "scale" if scl else ("factor" if fac else ("res" if res else "streaming")),
+             "cycles": dict(zip(SEG_SCL if scl else (SEG_FAC if fac else (SEG_RES if res else SEG)), d)),
              "total": (t[ns] - t[0]) if t[ns] and t[0] else None}
         rows.append(r)
         print(json.dumps(r), flush=True)
