@@ -23,8 +23,11 @@ def test_scan_flags_back_to_back_shrinking_masks():
 	v_fmac_f64_dpp v[14:15], v[2:3], v[8:9] row_newbcast:8 row_mask:0xf bank_mask:0xc
 	v_add_f64 v[16:17], v[0:1], v[0:1]
 	v_fmac_f64_dpp v[16:17], v[2:3], v[8:9] row_newbcast:8 row_mask:0x3 bank_mask:0xf
+	v_mov_b32 v20, v0
+	v_mov_b32_dpp v21, v20 row_shr:1 row_mask:0xf bank_mask:0xf
 """
-    seen, hazards = dhs.scan_text(asm)
+    seen, hazards, src = dhs.scan_text(asm)
+    assert [h[1].split()[0] for h in src] == ["v_mov_b32_dpp"]
     assert seen == 4
     # the second (right after a write of v[12:13]) and the last (right after v_add wrote v[16:17])
     assert [h[1].split()[1] for h in hazards] == ["v[12:13],", "v[16:17],"]
@@ -36,3 +39,4 @@ def test_release_library_has_no_dpp_mask_hazard():
     r = dhs.scan(LIB)
     assert r["partial_mask_dpp_fma"] > 0, r  # the scan sees the sweeps' triangular products
     assert r["hazards"] == 0, r
+    assert r["dpp_source_hazards"] == 0, r
