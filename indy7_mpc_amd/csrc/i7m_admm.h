@@ -1907,6 +1907,7 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
   for (int e = l; e < T; e += 64) so_[e] = D[e] * sX[e];
 }
 
+#ifndef I7M_ADMM_PREP_IN_TU  // (i7m_api.hip: these two live in i7m_admm_prep_tu.hip, built with max-ILP)
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_SCALE_WPE, I7M_ADMM_SCALE_WPE)))
 k_admm_scale(AdmmArgs a) {
@@ -1916,11 +1917,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
 }
+#endif
 // four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {
   admm_iter4<ADAPT>(a);
 }
+#ifndef I7M_ADMM_PREP_ONLY  // (i7m_admm_prep_tu.hip: no copies of the iteration kernels)
 // two problems per wave (grid = ceil(problems / 2)): a 21 KB ring, two waves per SIMD possible.  Per
 // problem the same arithmetic (bit-identical); a step issues 7 DMA wave-instructions instead of 13,
 // so a wave's step is shorter when the batch is small (launches of <= 512 problems use it), while
@@ -1932,5 +1935,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter_res(AdmmArgs a) {
   admm_iter_res<ARES_N>(a);
 }
+#endif
 
 }  // namespace i7m

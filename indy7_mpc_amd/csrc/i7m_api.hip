@@ -22,6 +22,7 @@
 #include "i7m_linearize.h"
 #include "i7m_riccati_mfma.h"
 #include "i7m_box.h"
+#define I7M_ADMM_PREP_IN_TU 1  // k_admm_scale / k_admm_factor: i7m_admm_prep_tu.hip
 #include "i7m_admm.h"
 #include "i7m_mpc.h"
 
@@ -43,6 +44,10 @@ void i7m_launch_linearize_kernel(bool spec, int grid, hipStream_t s, hipEvent_t 
                                  const void* params, const double* xu, const double* goals, const double* fext,
                                  bool fext_world, const int* active, double* lin, double* cost, double* qpd,
                                  int* init_active, void* init_stats);
+
+// i7m_admm_prep_tu.hip (the ADMM scaling and factor kernels under the max-ILP scheduler): kernel 0
+// k_admm_scale<9>, 1 k_admm_scale<18>, 2 k_admm_factor; args: const AdmmArgs*
+hipError_t i7m_launch_admm_prep(int kernel, int grid, hipStream_t s, hipEvent_t ea, hipEvent_t eb, const void* args);
 
 // i7m_fused_tu.hip (k_sqp_fused in a unit of its own)
 hipError_t i7m_launch_sqp_fused(bool spec, int W, bool fext_world, int it, hipStream_t s, hipEvent_t ea, hipEvent_t eb,
@@ -559,15 +564,12 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
       const int n = std::min(chunk, P.B - lo);
       int rc2 = timed(h, s, I7M_K_ADMM_PREP, [&](hipEvent_t ea, hipEvent_t eb) {
         // scaling, then the factor (one event pair around both)
-        if (P.N <= 32)
-          hipExtLaunchKernelGGL(k_admm_scale<9>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
-        else
-          hipExtLaunchKernelGGL(k_admm_scale<18>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
+        (void)i7m_launch_admm_prep(P.N <= 32 ? 0 : 1, n, s, ea, nullptr, &a);
         if (h->mark_ev && h->admm_stagger == 4) {  // (A/B: the mark between scaling and factor)
           (void)hipEventRecord(h->mark_ev, s);
           h->mark_ev = nullptr;
         }
-        hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
+        (void)i7m_launch_admm_prep(2, n, s, nullptr, eb, &a);
       });
       if (rc2) return rc2;
       if (h->mark_ev && h->admm_stagger == 1) {
@@ -1003,7 +1005,10 @@ const char* i7m_last_error(void) { return g_err.c_str(); }
 // Diagnostic library only (not declared in include/indy7_mpc.h): point every instrumented
 // kernel of both translation units at a per-wave timeline buffer (i7m_timeline.h; nullptr: off).
 int i7m_lin_tu_set_timeline(void* p);
-int i7m_diag_timeline(void* p) { return (i7m::tl_set(p) == 0 && i7m_lin_tu_set_timeline(p) == 0) ? 0 : -1; }
+int i7m_admm_prep_tu_set_timeline(void* p);
+int i7m_diag_timeline(void* p) {
+  return (i7m::tl_set(p) == 0 && i7m_lin_tu_set_timeline(p) == 0 && i7m_admm_prep_tu_set_timeline(p) == 0) ? 0 : -1;
+}
 #endif
 
 int i7m_abi_version(void) { return I7M_ABI_VERSION; }
