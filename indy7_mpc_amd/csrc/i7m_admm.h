@@ -1907,7 +1907,6 @@ __device__ __forceinline__ void admm_iter_res(const AdmmArgs& a) {
   for (int e = l; e < T; e += 64) so_[e] = D[e] * sX[e];
 }
 
-#ifndef I7M_ADMM_PREP_IN_TU  // (i7m_api.hip: these two live in i7m_admm_prep_tu.hip, built with max-ILP)
 template <int CT>  // columns of [P; A] per lane: 9 for N <= 32, 18 for N <= 64
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADMM_SCALE_WPE, I7M_ADMM_SCALE_WPE)))
 k_admm_scale(AdmmArgs a) {
@@ -1917,7 +1916,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(I7M_ADM
 k_admm_factor(AdmmArgs a) {
   admm_body<8, 1>(a);
 }
-#endif
 // four problems per wave (grid = ceil(problems / 4))
 template <bool ADAPT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) k_admm_iter(AdmmArgs a) {

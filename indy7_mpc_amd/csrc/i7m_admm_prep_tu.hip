@@ -4,10 +4,12 @@
 // unit (profiles/r06zm_sched_maxilp_ab.txt): the scaling + factor 352 -> 330 us per QP at B = 1,
 // 356 -> 334 at B = 64, 1102-1122 -> 1067-1086 at B = 4096, bit-identical, while the same flag
 // makes k_admm_iter 3-4 % longer at config 3 and leaves k_admm_iter_res level — hence the split.
+// i7m_api.hip keeps its own default-scheduled copies for the staggered ranges of config 3, where
+// these make the step 0.6 % longer (profiles/r06zo; i7m_handle::admm_prep_ilp picks by size).
 //
 // i7m_admm.h included inside an anonymous namespace: this unit's kernels and device functions stay
-// internal (i7m_api.hip defines I7M_ADMM_PREP_IN_TU, so its copy of the header defines neither
-// kernel).  The launcher is the only external symbol, with builtin parameter types only.
+// internal (I7M_ADMM_PREP_ONLY: no copies of the iteration kernels).  The launcher is the only
+// external symbol, with builtin parameter types only.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 

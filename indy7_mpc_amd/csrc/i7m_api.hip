@@ -22,7 +22,6 @@
 #include "i7m_linearize.h"
 #include "i7m_riccati_mfma.h"
 #include "i7m_box.h"
-#define I7M_ADMM_PREP_IN_TU 1  // k_admm_scale / k_admm_factor: i7m_admm_prep_tu.hip
 #include "i7m_admm.h"
 #include "i7m_mpc.h"
 
@@ -162,6 +161,12 @@ struct i7m_handle {
   // = 0 never, 1 whenever it fits, -1 (default) by that size
   int admm_res = -1;
   int admm_res_max = 256;
+  // k_admm_scale / k_admm_factor as built under the max-ILP scheduler (i7m_admm_prep_tu.hip) for
+  // launches of at most admm_prep_ilp_max problems, else this unit's: 6 % shorter at B <= 256, but
+  // at config 3 (staggered ranges of 2048) the step 0.6 % longer beside the other range's
+  // iteration (profiles/r06zn, r06zo); I7M_ADMM_PREP_ILP = 0 never, 1 always, -1 (default) by size
+  int admm_prep_ilp = -1;
+  int admm_prep_ilp_max = 1024;
   // extra dynamic LDS per k_admm_iter workgroup (I7M_ADMM_ITER_DYN_LDS, bytes; A/B): past 160 KB / 4
   // it leaves one SIMD of every CU, and its LDS, to the other range's kernels
   int admm_iter_dyn_lds = 0;
@@ -564,12 +569,22 @@ int solve_qp(i7m_handle* h, hipStream_t s, const Bufs& W, const SolveParams& P, 
       const int n = std::min(chunk, P.B - lo);
       int rc2 = timed(h, s, I7M_K_ADMM_PREP, [&](hipEvent_t ea, hipEvent_t eb) {
         // scaling, then the factor (one event pair around both)
-        (void)i7m_launch_admm_prep(P.N <= 32 ? 0 : 1, n, s, ea, nullptr, &a);
+        // the max-ILP-scheduled copies (i7m_admm_prep_tu.hip) or this unit's (default scheduler)
+        const bool ilp = h->admm_prep_ilp > 0 || (h->admm_prep_ilp < 0 && n <= h->admm_prep_ilp_max);
+        if (ilp)
+          (void)i7m_launch_admm_prep(P.N <= 32 ? 0 : 1, n, s, ea, nullptr, &a);
+        else if (P.N <= 32)
+          hipExtLaunchKernelGGL(k_admm_scale<9>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
+        else
+          hipExtLaunchKernelGGL(k_admm_scale<18>, dim3(n), dim3(64), 0, s, ea, nullptr, 0, a);
         if (h->mark_ev && h->admm_stagger == 4) {  // (A/B: the mark between scaling and factor)
           (void)hipEventRecord(h->mark_ev, s);
           h->mark_ev = nullptr;
         }
-        (void)i7m_launch_admm_prep(2, n, s, nullptr, eb, &a);
+        if (ilp)
+          (void)i7m_launch_admm_prep(2, n, s, nullptr, eb, &a);
+        else
+          hipExtLaunchKernelGGL(k_admm_factor, dim3(n), dim3(64), 0, s, nullptr, eb, 0, a);
       });
       if (rc2) return rc2;
       if (h->mark_ev && h->admm_stagger == 1) {
@@ -1150,6 +1165,8 @@ int i7m_create(const i7m_config* cfg, i7m_handle** out) {
   if (const char* e = std::getenv("I7M_ADMM_ITER2")) h->admm_iter2 = std::min(std::max(std::atoi(e), -1), 1);
   if (const char* e = std::getenv("I7M_ADMM_RES")) h->admm_res = std::min(std::max(std::atoi(e), -1), 1);
   if (const char* e = std::getenv("I7M_ADMM_RES_MAX")) h->admm_res_max = std::max(std::atoi(e), 0);
+  if (const char* e = std::getenv("I7M_ADMM_PREP_ILP")) h->admm_prep_ilp = std::min(std::max(std::atoi(e), -1), 1);
+  if (const char* e = std::getenv("I7M_ADMM_PREP_ILP_MAX")) h->admm_prep_ilp_max = std::max(std::atoi(e), 0);
   if (const char* e = std::getenv("I7M_ADMM_ITER_DYN_LDS")) h->admm_iter_dyn_lds = std::min(std::max(std::atoi(e), 0), 65536);
   if (h->h2h_chunks < 0 || h->h2h_chunks > 64) return bail(fail(I7M_EINVAL, "h2h_chunks must be in [0, 64]"));
   if (hipStreamCreateWithFlags(&h->cs[0], hipStreamNonBlocking) != hipSuccess ||
